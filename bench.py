@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""bench.py -- stencil_smi Jacobi GCell/s on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A "step" is one Jacobi timestep over the whole job's grid.  N=1 runs
+BASELINE config 2 (8192x8192 fp32 on one GPU, no halo exchange).  N>1 runs
+weak scaling with an 8192x8192 tile per GPU on the stencil_smi decomposition
+(1x2, 2x2, 2x4; rank = i_px*PY + i_py), halos exchanged every step through
+RCCL over xGMI, overlapped with the interior sweep.  Inputs are resident in
+HBM before the timed region; the timed region is exactly K steps bracketed by
+a barrier + device synchronize on both sides; the time is the max over ranks.
+
+The JSON line also carries:
+  roofline      -- the sweep kernel: algorithmic 8 B/cell per launch divided
+                   by its average duration (HIP events around every launch,
+                   on the launch stream, inside the timed region), vs the
+                   8 TB/s HBM3E peak; `traffic` is HBM bytes per launch from
+                   the rocprofv3 PMC pass committed under profiles/ (or null)
+  cpu_baseline  -- the oracle's C restatement of the reference stencil
+                   (OpenMP) timed on this host on a bounded sample (rank 0,
+                   N=1 only)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BYTES_PER_CELL = 8             # one fp32 read + one fp32 write per cell per step
+TILE = 8192                    # per-GPU tile edge (BASELINE config 2 / weak scaling)
+DECOMP = {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_stencil_sweep.json")
+
+
+def decomposition(n: int) -> tuple[int, int]:
+    if n in DECOMP:
+        return DECOMP[n]
+    px = int(np.sqrt(n))
+    while n % px:
+        px -= 1
+    return px, n // px
+
+
+def cpu_baseline(budget_s: float = 4.0) -> dict:
+    """Oracle (C restatement of the reference stencil, all host threads)."""
+    import oracle
+    threads = min(16, os.cpu_count() or 1)
+    g = oracle.init_uniform(TILE, TILE, seed=42)
+    t0 = time.perf_counter()
+    oracle.stencil(g, 1, threads=threads)
+    one = time.perf_counter() - t0
+    steps = max(1, min(40, int(budget_s / max(one, 1e-3))))
+    t0 = time.perf_counter()
+    oracle.stencil(g, steps, threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(TILE * TILE * steps / dt / 1e9, 3),
+        "unit": "GCell/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{TILE}x{TILE} fp32 Jacobi, {steps} steps, OpenMP C restatement "
+                  f"(oracle/smi_oracle.c) of stencil_smi.cl:117-165, {dt:.1f} s wall",
+    }
+
+
+def pmc_traffic(cells: int) -> float | None:
+    """HBM bytes per sweep launch from the committed rocprofv3 PMC summary,
+    if it was measured on this same per-GPU tile."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+        if int(d.get("cells", -1)) == cells:
+            return float(d["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--tile", type=int, default=TILE)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import smi_amd
+    from smi_amd import profiling, stencil
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    smi_amd.load()
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        comm = smi_amd.Comm.from_env(device=local)
+    else:
+        comm = smi_amd.LocalGroup(1, device=local).comm(0)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    PX, PY = decomposition(world)
+    X = Y = args.tile
+    g = np.random.default_rng(1000 + rank).random((X, Y), dtype=np.float32)
+    tile = torch.from_numpy(g).cuda()
+    scratch = torch.empty_like(tile)
+    stream = torch.cuda.Stream()
+
+    with torch.cuda.stream(stream):
+        if args.warmup:
+            stencil.run(comm, tile, args.warmup, PX, PY, scratch)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        profiling.reset()
+        profiling.enable(True)
+        t0 = time.perf_counter()
+        stencil.run(comm, tile, args.steps, PX, PY, scratch)
+        torch.cuda.synchronize()
+        barrier()
+        t1 = time.perf_counter()
+        profiling.enable(False)
+    elapsed = t1 - t0
+    sweep_ms, sweep_n = profiling.read(profiling.SWEEP)
+    edge_ms, edge_n = profiling.read(profiling.EDGE)
+    if world > 1:
+        t = torch.tensor([elapsed, sweep_ms / max(sweep_n, 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, sweep_avg_ms = float(t[0]), float(t[1])
+    else:
+        sweep_avg_ms = sweep_ms / max(sweep_n, 1)
+
+    cells_per_gpu = X * Y
+    total_cells = cells_per_gpu * world
+    value = total_cells * args.steps / elapsed / 1e9
+    achieved = BYTES_PER_CELL * cells_per_gpu / (sweep_avg_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(cells_per_gpu)
+    out = {
+        "metric": "Jacobi stencil GCell/s (8192^2 fp32 per GPU)",
+        "value": round(value, 2),
+        "unit": "GCell/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (uniform [0,1) fp32 grid, seed 1000+rank)",
+        "config": {
+            "workload": f"stencil_smi 4-point Jacobi, {X}x{Y} fp32 tile per GPU, "
+                        f"{PX}x{PY} decomposition ({PX * X}x{PY * Y} global)"
+                        + (", halo exchange over RCCL/xGMI overlapped with the interior" if world > 1
+                           else ", no halo exchange (BASELINE config 2)"),
+            "grid": [PX * X, PY * Y],
+            "tile": [X, Y],
+            "decomposition": [PX, PY],
+            "tuning": stencil.get_tuning(),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "sweep_kernel (smi_amd/csrc/stencil.hip)",
+            "kernel_avg_ms": round(sweep_avg_ms, 5),
+            "launches": sweep_n,
+            "bytes_per_launch": BYTES_PER_CELL * cells_per_gpu,
+        },
+    }
+    if edge_n:
+        out["roofline"]["edge_kernel_avg_ms"] = round(edge_ms / edge_n, 5)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    comm.finalize()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,70 @@
+/*
+ * communicator.h -- communicator and runtime bring-up.
+ *
+ * Replaces:
+ *   - SMI_Comm = char2{rank, size} and SMI_Comm_rank/SMI_Comm_size
+ *     (include/smi/communicator.h:12-31);
+ *   - the generated host initialiser SMI_Comm SmiInit_<program>(rank,
+ *     ranks_count, routing_dir, context, program, buffers)
+ *     (codegen/templates/host_hlslib.cl:8-90), which loaded routing tables
+ *     and launched the never-terminating CK_S/CK_R/support kernels.
+ * On one 8xMI355X node there is nothing to route: rank r drives GPU r and
+ * every pair of GPUs is one xGMI hop, so initialisation is just an RCCL
+ * communicator (or, for single-GPU testing, an in-process group whose ranks
+ * are host threads sharing one device).
+ */
+#ifndef SMI_COMMUNICATOR_H
+#define SMI_COMMUNICATOR_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Opaque stream handle (a hipStream_t; NULL = the device's null stream). */
+typedef void *SMI_Stream;
+
+/* Communicator, passed by value like the reference's char2.  `handle`
+ * indexes the runtime's table of live communicators. */
+typedef struct {
+    int rank;
+    int size;
+    int handle;
+} SMI_Comm;
+
+static inline int SMI_Comm_rank(SMI_Comm comm) { return comm.rank; }
+static inline int SMI_Comm_size(SMI_Comm comm) { return comm.size; }
+
+#define SMI_UNIQUE_ID_BYTES 128
+
+/* Fill `id` (SMI_UNIQUE_ID_BYTES bytes) with a fresh RCCL unique id; call on
+ * rank 0 and distribute the bytes to every rank (the Python host uses the
+ * torch.distributed store). */
+int smi_get_unique_id(void *id, int id_bytes);
+
+/* One process per GPU: RCCL communicator over xGMI.  Selects `device` for
+ * the calling thread.  Collective: every rank must call it. */
+int smi_init(int rank, int size, int device, const void *unique_id, int id_bytes,
+             SMI_Comm *comm);
+
+/* In-process group: `size` ranks are host threads of this process (all on
+ * `device` or on devices of their own).  smi_local_group_create returns a
+ * group id; each rank thread then calls smi_init_local with it.  Transfers
+ * are device-to-device copies ordered by HIP events -- a GPU transport used
+ * to run multi-rank parity tests on a single GPU. */
+int smi_local_group_create(int size, int *group_id);
+int smi_init_local(int group_id, int rank, int device, SMI_Comm *comm);
+
+int smi_finalize(SMI_Comm comm);
+
+/* Devices visible to this process. */
+int smi_device_count(int *count);
+
+/* Block until all work queued on `stream` has finished. */
+int smi_stream_synchronize(SMI_Stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMI_COMMUNICATOR_H */

@@ -1,0 +1,34 @@
+/*
+ * profiling.h -- live per-kernel timing with HIP events.
+ *
+ * The reference times whole kernel sets with std::chrono or OpenCL events
+ * (examples/host/stencil_smi.cpp:316-340, microbenchmarks/host/
+ * reduce_benchmark.cpp:120-155).  Here, while enabled, every launch of the
+ * named hot kernel is bracketed by a pair of hipEvents recorded on the
+ * stream it is launched on; smi_prof_read returns the summed duration.
+ */
+#ifndef SMI_PROFILING_H
+#define SMI_PROFILING_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    SMI_PROF_STENCIL_SWEEP = 0,  /* the Jacobi sweep kernel                */
+    SMI_PROF_STENCIL_EDGE = 1,   /* halo-edge kernel (multi-rank overlap)  */
+    SMI_PROF_REDUCE_FOLD = 2,
+    SMI_PROF_GEMV = 3,
+    SMI_PROF_NUM = 4
+} SMI_ProfKernel;
+
+int smi_prof_enable(int enable);
+int smi_prof_reset(void);
+/* Synchronises the recorded events; *total_ms = summed kernel time,
+ * *launches = number of timed launches of `kernel`. */
+int smi_prof_read(int kernel, double *total_ms, long *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMI_PROFILING_H */

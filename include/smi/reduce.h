@@ -1,0 +1,51 @@
+/*
+ * reduce.h -- SMI_Reduce on whole buffers.
+ *
+ * Replaces SMI_Open_reduce_channel / SMI_Reduce (include/smi/reduce.h:55-76)
+ * and the root-side support kernel smi_kernel_reduce_<port>
+ * (codegen/templates/reduce.cl:3-245), which reduced one element per 32-byte
+ * packet with a 16-deep credit window.
+ *
+ * Arithmetic contract: for every element the contributions are folded in
+ * rank order through an S-slot rotating accumulator (S = 4 for float/double,
+ * 1 for int/short/char, codegen/ops.py:110-116; init 0 / *_MIN / *_MAX,
+ * codegen/ops.py:124-141):  q[S] = op(d_k, q[0]); shift; then
+ * result = op(...op(init, q[0])..., q[S-1])  (reduce.cl:65-69,100-105,120-125).
+ * Integer types wrap.  The result is defined on `root` only.
+ */
+#ifndef SMI_REDUCE_H
+#define SMI_REDUCE_H
+
+#include <stddef.h>
+#include "communicator.h"
+#include "data_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same enumerators and values as include/smi/reduce.h:18-22. */
+typedef enum {
+    SMI_ADD = 0,
+    SMI_MAX = 1,
+    SMI_MIN = 2
+} SMI_Op;
+
+/* Reduce `count` elements of every rank's device buffer `sendbuf` into the
+ * root's device buffer `recvbuf` (ignored on other ranks).  `port` tags the
+ * operation like the reference's logical port (ops on different ports may be
+ * issued from different host threads).  Enqueued on `stream`. */
+int smi_reduce(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count,
+               SMI_Datatype type, SMI_Op op, int root, int port,
+               SMI_Stream stream);
+
+/* The local fold kernel: contribs holds `nranks` rows of `count` elements
+ * (row r = rank r's contribution, row pitch `ld` elements); out[i] = fold of
+ * column i in row order.  Used by smi_reduce on each chunk owner. */
+int smi_reduce_fold(const void *contribs, void *out, int nranks, size_t count,
+                    size_t ld, SMI_Datatype type, SMI_Op op, SMI_Stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMI_REDUCE_H */

@@ -1,0 +1,72 @@
+/*
+ * stencil.h -- the stencil_smi hot path: 4-point Jacobi with streamed halos.
+ *
+ * Replaces the stencil_smi application's device pipeline
+ *   Read / Stencil / Write            examples/kernels/stencil_smi.cl:20-234
+ *   Convert{Send,Receive}{Top,Bottom,Left,Right}
+ *                                     examples/kernels/stencil_smi.cl:236-386
+ * and the host decomposition (rank = i_px*PY + i_py, tile rows
+ * [i_px*X_LOCAL, ..), cols [i_py*Y_LOCAL, ..))
+ *                                     examples/host/stencil_smi.cpp:48-62,133-134
+ * Arithmetic contract (bit-exact): interior cell
+ *   out = 0.25f * (((S + W) + E) + N)    S=x[i+1][j] W=x[i][j-1] E=x[i][j+1] N=x[i-1][j]
+ * in IEEE fp32 round-to-nearest with no contraction (stencil_smi.cl:153-156);
+ * cells on the global edge are copied unchanged (stencil_smi.cl:143-151).
+ *
+ * Layout: a rank's tile is x_local rows of y_local fp32, row-major, dense
+ * (row pitch = y_local), 16-byte aligned; y_local must be a multiple of 4.
+ */
+#ifndef SMI_STENCIL_H
+#define SMI_STENCIL_H
+
+#include "communicator.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* How a tile side is treated by one sweep. */
+typedef enum {
+    SMI_SIDE_COPY = 0,  /* side lies on the global edge: copy its cells      */
+    SMI_SIDE_HALO = 1,  /* neighbour values come from the halo vector        */
+    SMI_SIDE_SKIP = 2   /* leave the side's cells unwritten (computed apart) */
+} SMI_SideMode;
+
+/* Side order in the arrays below. */
+enum { SMI_TOP = 0, SMI_BOTTOM = 1, SMI_LEFT = 2, SMI_RIGHT = 3 };
+
+/* One Jacobi step of one tile, enqueued on `stream`.
+ *   halo[SMI_TOP] / halo[SMI_BOTTOM]: y_local values of the row above / below
+ *   halo[SMI_LEFT] / halo[SMI_RIGHT]: x_local values of the column left/right
+ * (required, i.e. non-NULL, exactly for sides in SMI_SIDE_HALO mode).
+ * send_left / send_right (nullable) receive the tile's new first / last
+ * column, packed -- the fused equivalent of Write's tee into send_left /
+ * send_right (stencil_smi.cl:201-224).  `in` and `out` must not overlap. */
+int smi_stencil_step(const float *in, float *out, int x_local, int y_local,
+                     const int mode[4], const float *const halo[4],
+                     float *send_left, float *send_right, SMI_Stream stream);
+
+/* Full run of the stencil_smi program on this rank's tile: `timesteps`
+ * Jacobi steps over the PX x PY decomposition of `comm` (PX*PY == size),
+ * halos exchanged every step with the four neighbours through RCCL on a
+ * dedicated stream, overlapped with the interior sweep.  buf0 holds the
+ * initial tile; buf1 is scratch of the same size.  On return *result_index
+ * (0 or 1) names the buffer holding the final tile (like the reference's
+ * half timesteps%2, stencil_smi.cpp:344).  Asynchronous w.r.t. the host
+ * except for transport rendezvous. */
+int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local,
+                    int y_local, int px, int py, int timesteps,
+                    SMI_Stream stream, int *result_index);
+
+/* Tuning knobs of the sweep kernel (row-block height, rows in flight per
+ * wave, non-temporal stores, 1 = overlap halo exchange with the interior).
+ * Pass <= 0 / < 0 to keep a value.  Bit-exact results for every setting. */
+int smi_stencil_set_tuning(int rows_per_wave, int rows_in_flight,
+                           int nontemporal_stores, int overlap);
+int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
+                           int *nontemporal_stores, int *overlap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMI_STENCIL_H */

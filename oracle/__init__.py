@@ -1,0 +1,245 @@
+"""CPU oracle for the SMI hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this package, and only as the checker or as
+the timed CPU baseline.  The product (``smi_amd``) never imports it and fails
+loudly when its HIP library is missing.
+
+The arithmetic lives in ``smi_oracle.c`` (plain C, built by ``Makefile`` with
+``-ffp-contract=off``); this module is a thin numpy/ctypes wrapper plus a few
+pure-Python restatements used to pin the C code on small cases:
+
+* :func:`stencil_exact` -- exact rational Jacobi (``fractions.Fraction``) used
+  to pin the C stencil bit-for-bit on the steps where every value is a short
+  dyadic rational (any summation order gives the same bits there).
+* :func:`reduce_fold_py` -- a loop restatement of the root-side reduce fold of
+  ``codegen/templates/reduce.cl:42-148`` used to cross-check the C fold.
+
+Parity status per path is recorded in DESIGN.md ("Oracle").
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from fractions import Fraction
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libsmi_oracle.so")
+_lib = None
+
+# include/smi/data_types.h:10-16
+SMI_INT, SMI_FLOAT, SMI_DOUBLE, SMI_CHAR, SMI_SHORT = 1, 2, 3, 4, 5
+# include/smi/reduce.h:18-22
+SMI_ADD, SMI_MAX, SMI_MIN = 0, 1, 2
+
+NP_DTYPE = {
+    SMI_INT: np.int32,
+    SMI_FLOAT: np.float32,
+    SMI_DOUBLE: np.float64,
+    SMI_CHAR: np.int8,
+    SMI_SHORT: np.int16,
+}
+
+# codegen/ops.py:110-116 -- SHIFT_REG per data type
+SHIFT_REG = {SMI_DOUBLE: 4, SMI_FLOAT: 4, SMI_INT: 1, SMI_SHORT: 1, SMI_CHAR: 1}
+
+
+def build(force: bool = False) -> str:
+    """Compile smi_oracle.c with the committed Makefile (gcc)."""
+    if force or not os.path.exists(_LIB_PATH) or (
+        os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "smi_oracle.c"))
+    ):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        I = ctypes.c_int
+        _lib.oracle_stencil.argtypes = [P, P, I, I, I, I, I]
+        _lib.oracle_stencil_decomposed.argtypes = [P, P, I, I, I, I, I]
+        _lib.oracle_reduce.argtypes = [P, P, I, ctypes.c_long, I, I, P]
+        _lib.oracle_gesummv.argtypes = [P, P, P, P, I, I, ctypes.c_float, ctypes.c_float, I]
+        for f in ("oracle_stencil", "oracle_stencil_decomposed", "oracle_reduce",
+                  "oracle_gesummv", "oracle_max_threads"):
+            getattr(_lib, f).restype = ctypes.c_int
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+# ---------------------------------------------------------------- stencil --
+def init_edges(X: int, Y: int) -> np.ndarray:
+    """Reference test pattern: 0 interior, 1 on all four edges
+    (examples/host/stencil_smi.cpp:175-187)."""
+    g = np.zeros((X, Y), dtype=np.float32)
+    g[0, :] = 1
+    g[X - 1, :] = 1
+    g[:, 0] = 1
+    g[:, Y - 1] = 1
+    return g
+
+
+def init_uniform(X: int, Y: int, seed: int = 42) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    return rng.random((X, Y), dtype=np.float32)
+
+
+def stencil(grid: np.ndarray, T: int, order: str = "device", threads: int = 0) -> np.ndarray:
+    """T Jacobi steps.  order='device' is the stencil_smi.cl:153-156 order
+    (S+W+E+N); order='host' is the reference host Reference() order
+    (N+S+W+E, stencil_smi.cpp:33-46)."""
+    g = np.ascontiguousarray(grid, dtype=np.float32)
+    out = np.empty_like(g)
+    X, Y = g.shape
+    rc = lib().oracle_stencil(_ptr(g), _ptr(out), X, Y, T, 0 if order == "device" else 1, threads)
+    if rc:
+        raise ValueError(f"oracle_stencil rc={rc}")
+    return out
+
+
+def stencil_decomposed(grid: np.ndarray, T: int, PX: int, PY: int) -> np.ndarray:
+    """Rank-decomposed emulation of the stencil_smi program (Read/Stencil/
+    Write per rank with halo queues, stencil_smi.cl:20-386)."""
+    g = np.ascontiguousarray(grid, dtype=np.float32)
+    out = np.empty_like(g)
+    X, Y = g.shape
+    rc = lib().oracle_stencil_decomposed(_ptr(g), _ptr(out), X, Y, PX, PY, T)
+    if rc:
+        raise ValueError(f"oracle_stencil_decomposed rc={rc}")
+    return out
+
+
+def stencil_exact(grid, T: int):
+    """Exact rational Jacobi (no rounding at all) -- pins the fp32 oracle
+    while every intermediate is exactly representable."""
+    X = len(grid)
+    Y = len(grid[0])
+    cur = [[Fraction(float(v)) for v in row] for row in grid]
+    q = Fraction(1, 4)
+    for _ in range(T):
+        nxt = [row[:] for row in cur]
+        for i in range(1, X - 1):
+            for j in range(1, Y - 1):
+                nxt[i][j] = q * (cur[i + 1][j] + cur[i][j - 1] + cur[i][j + 1] + cur[i - 1][j])
+        cur = nxt
+    return cur
+
+
+def reference_check(result: np.ndarray, reference: np.ndarray) -> bool:
+    """The reference host's acceptance test: |ref - res| < 1e-4 * mean(ref)
+    for every cell (examples/host/stencil_smi.cpp:391-405; the mean is
+    accumulated in double and stored as Data_t=float)."""
+    average = np.float32(np.sum(reference, dtype=np.float64) / reference.size)
+    diff = np.abs(reference.astype(np.float32) - result.astype(np.float32))
+    return bool(np.all(diff < 1e-4 * float(average)))
+
+
+# ----------------------------------------------------------------- reduce --
+def reduce(contribs: np.ndarray, dtype: int, op: int, arrival=None) -> np.ndarray:
+    """Root-side reduce fold (codegen/templates/reduce.cl:42-148).
+    contribs: (nranks, count) array, row r = rank r's send buffer."""
+    npdt = NP_DTYPE[dtype]
+    c = np.ascontiguousarray(contribs, dtype=npdt)
+    n, count = c.shape
+    out = np.empty(count, dtype=npdt)
+    arr = None
+    arr_ptr = None
+    if arrival is not None:
+        arr = np.ascontiguousarray(arrival, dtype=np.int32)
+        arr_ptr = _ptr(arr)
+    rc = lib().oracle_reduce(_ptr(c), _ptr(out), n, count, dtype, op, arr_ptr)
+    if rc:
+        raise ValueError(f"oracle_reduce rc={rc}")
+    return out
+
+
+def _init_value(dtype: int, op: int):
+    """codegen/ops.py:124-141 SHIFT_REG_INIT."""
+    npdt = NP_DTYPE[dtype]
+    if op == SMI_ADD:
+        return npdt(0)
+    if dtype in (SMI_FLOAT, SMI_DOUBLE):
+        fi = np.finfo(npdt)
+        return npdt(fi.tiny) if op == SMI_MAX else npdt(fi.max)  # FLT_MIN / FLT_MAX
+    ii = np.iinfo(npdt)
+    return npdt(ii.min) if op == SMI_MAX else npdt(ii.max)
+
+
+def reduce_fold_py(values, dtype: int, op: int):
+    """Pure-Python loop restatement of one element's fold, in the given
+    arrival order (reduce.cl:65-69, 100-105, 120-125)."""
+    npdt = NP_DTYPE[dtype]
+    S = SHIFT_REG[dtype]
+    init = _init_value(dtype, op)
+
+    def apply(a, b):
+        if op == SMI_ADD:
+            return _wrap_add(a, b, npdt)
+        if op == SMI_MAX:
+            return a if a > b else b
+        return a if a < b else b
+
+    q = [init] * (S + 1)
+    for d in values:
+        q[S] = apply(npdt(d), q[0])
+        for j in range(S):
+            q[j] = q[j + 1]
+    res = init
+    for j in range(S):
+        res = apply(res, q[j])
+    return npdt(res)
+
+
+def _wrap_add(a, b, npdt):
+    if np.issubdtype(npdt, np.floating):
+        return npdt(npdt(a) + npdt(b))
+    bits = 8 * np.dtype(npdt).itemsize
+    s = (int(a) + int(b)) & ((1 << bits) - 1)
+    if s >= 1 << (bits - 1):
+        s -= 1 << bits
+    return npdt(s)
+
+
+# ---------------------------------------------------------------- gesummv --
+def gesummv(A: np.ndarray, B: np.ndarray, x: np.ndarray, alpha: float, beta: float,
+            threads: int = 0) -> np.ndarray:
+    """y = alpha*A*x + beta*B*x with the row-streamed fold of
+    examples/kernels/gesummv_rank0.cl:53-203."""
+    A = np.ascontiguousarray(A, dtype=np.float32)
+    B = np.ascontiguousarray(B, dtype=np.float32)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    N, M = A.shape
+    y = np.empty(N, dtype=np.float32)
+    rc = lib().oracle_gesummv(_ptr(A), _ptr(B), _ptr(x), _ptr(y), N, M,
+                              ctypes.c_float(alpha), ctypes.c_float(beta), threads)
+    if rc:
+        raise ValueError(f"oracle_gesummv rc={rc}")
+    return y
+
+
+def gesummv_reference_check(result: np.ndarray, A, B, x, alpha, beta) -> bool:
+    """The reference host's acceptance test (gesummv_smi.cpp:40-46,299-313):
+    rel. err < 1e-4 against sgemv(beta,B) then sgemv(alpha,A,+y); here the
+    BLAS is replaced by a float64 evaluation of the same expression."""
+    ref = (beta * (B.astype(np.float64) @ x.astype(np.float64))
+           + alpha * (A.astype(np.float64) @ x.astype(np.float64))).astype(np.float32)
+    res = result.astype(np.float32)
+    ok = np.isfinite(res) & np.isfinite(ref)
+    both_zero = (res == 0) & (ref == 0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rel = np.abs(res - ref) / np.abs(ref)
+    return bool(np.all(ok & (both_zero | (rel < 1e-4))))
+
+
+def max_threads() -> int:
+    return int(lib().oracle_max_threads())

@@ -1,0 +1,376 @@
+/*
+ * smi_oracle.c -- CPU restatement of the SMI hot-path arithmetic.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in smi_amd/ links, loads or calls this
+ * file.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * use it, and only as the checker / the timed CPU baseline.
+ *
+ * Every function cites the reference (ryutakashino/SMI, read-only at
+ * /root/reference) file:line whose behaviour it restates.  Build with
+ * -ffp-contract=off and without -ffast-math (oracle/Makefile does): the
+ * stencil and the reduce fold are defined by their exact summation order.
+ *
+ * Parity pinning (see DESIGN.md section "Oracle"):
+ *   - reduce / bcast / p2p: pinned by the reference's own known-answer tests
+ *     (test/reduce/reduce.cl, test/broadcast/broadcast.cl, test/p2p/p2p_rank{0,1}.cl,
+ *     microbenchmarks/kernels/reduce.cl), replayed in tests/test_oracle.py.
+ *   - stencil: pinned by exact rational arithmetic for the steps where every
+ *     value is a short dyadic rational, and by the reference host's own
+ *     acceptance check (|ref-res| < 1e-4*mean vs Reference(),
+ *     examples/host/stencil_smi.cpp:391-405) at 32 steps.  The bit order past
+ *     that point (S+W+E+N) is the device kernel's source order and is not
+ *     pinned by any reference fixture (none exists).
+ *   - gesummv: pinned by the reference host check (rel. err < 1e-4 vs two
+ *     sgemv calls, examples/host/gesummv_smi.cpp:40-46,299-313).
+ */
+#include <float.h>
+#include <limits.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* include/smi/data_types.h:10-16 */
+enum { OR_INT = 1, OR_FLOAT = 2, OR_DOUBLE = 3, OR_CHAR = 4, OR_SHORT = 5 };
+/* include/smi/reduce.h:18-22 */
+enum { OR_ADD = 0, OR_MAX = 1, OR_MIN = 2 };
+
+/* ------------------------------------------------------------------------ */
+/* Stencil                                                                   */
+/* ------------------------------------------------------------------------ */
+
+/* One interior cell in the device kernel's order:
+ * res = 0.25 * (S + W + E + N)     examples/kernels/stencil_smi.cl:153-156
+ * (S = buffer[2*(...)], the row streamed last; W/E = centre row -1/+1;
+ *  N = buffer[b*W+w], the row streamed first; the labels are confirmed by
+ *  examples/kernels/stencil_onchip_pe.cl.in:132-135).  The sum is evaluated
+ * left to right in fp32; 0.25 is a double literal (cl_khr_fp64), so the
+ * product is formed in double and rounded to float once -- identical to an
+ * fp32 multiply because the scaling by 0.25 is exact. */
+static inline float cell_device(float s, float w, float e, float n) {
+    float sum = s + w;
+    sum = sum + e;
+    sum = sum + n;
+    return (float)(0.25 * (double)sum);
+}
+
+/* The reference host's Reference() order: 0.25f * (N + S + W + E)
+ * examples/host/stencil_smi.cpp:33-46. */
+static inline float cell_host(float s, float w, float e, float n) {
+    float sum = n + s;
+    sum = sum + w;
+    sum = sum + e;
+    return 0.25f * sum;
+}
+
+/* One full-grid Jacobi step with global-edge cells copied unchanged
+ * (stencil_smi.cl:143-151 for the device, stencil_smi.cpp:36-37 for the
+ * host).  order: 0 = device (S+W+E+N), 1 = host Reference (N+S+W+E). */
+static void jacobi_step(const float *in, float *out, int X, int Y, int order) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < X; ++i) {
+        const float *c = in + (size_t)i * Y;
+        float *o = out + (size_t)i * Y;
+        if (i == 0 || i == X - 1) {
+            memcpy(o, c, sizeof(float) * (size_t)Y);
+            continue;
+        }
+        const float *n = c - Y;
+        const float *s = c + Y;
+        o[0] = c[0];
+        if (order == 0) {
+            for (int j = 1; j < Y - 1; ++j)
+                o[j] = cell_device(s[j], c[j - 1], c[j + 1], n[j]);
+        } else {
+            for (int j = 1; j < Y - 1; ++j)
+                o[j] = cell_host(s[j], c[j - 1], c[j + 1], n[j]);
+        }
+        if (Y > 1) o[Y - 1] = c[Y - 1];
+    }
+}
+
+/* T Jacobi steps over a full X*Y grid; result written to `out`.
+ * Restates the reference host Reference() loop structure
+ * (stencil_smi.cpp:33-46) with the chosen per-cell order. */
+int oracle_stencil(const float *in, float *out, int X, int Y, int T, int order,
+                   int threads) {
+    if (X <= 0 || Y <= 0 || T < 0) return -1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+    size_t n = (size_t)X * Y;
+    float *a = (float *)malloc(n * sizeof(float));
+    float *b = (float *)malloc(n * sizeof(float));
+    if (!a || !b) { free(a); free(b); return -2; }
+    memcpy(a, in, n * sizeof(float));
+    for (int t = 0; t < T; ++t) {
+        jacobi_step(a, b, X, Y, order);
+        float *tmp = a; a = b; b = tmp;
+    }
+    memcpy(out, a, n * sizeof(float));
+    free(a);
+    free(b);
+    return 0;
+}
+
+/* Rank-decomposed restatement of the stencil_smi emulator program:
+ *   host SplitMemory / rank map        stencil_smi.cpp:48-62, 133-134
+ *   Read  (tile + 1-cell halo ring, -100 dummies, corners unused)
+ *                                       stencil_smi.cl:20-115
+ *   Stencil (artificial t=0 pass-through, global-edge copy, S+W+E+N)
+ *                                       stencil_smi.cl:117-165
+ *   Write (ping-pong halves, halo tee to the four neighbours when t<T)
+ *                                       stencil_smi.cl:167-234
+ *   Convert{Send,Receive}* neighbour ranks (i_px+-1)*PY+i_py, i_px*PY+i_py+-1
+ *                                       stencil_smi.cl:236-386
+ * Every rank keeps its own (X_LOCAL+2) x (Y_LOCAL+2) extended tile; the halo
+ * queues are modelled as per-rank buffers filled from the neighbours' Write
+ * output of the previous timestep.  The result is recombined with
+ * CombineMemory (stencil_smi.cpp:80-93). */
+int oracle_stencil_decomposed(const float *in, float *out, int X, int Y, int PX,
+                              int PY, int T) {
+    if (PX <= 0 || PY <= 0 || X % PX || Y % PY || T < 0) return -1;
+    const int XL = X / PX, YL = Y / PY, XE = XL + 2, YE = YL + 2;
+    const int R = PX * PY;
+    float *tile = (float *)malloc(sizeof(float) * (size_t)R * XL * YL);
+    float *next = (float *)malloc(sizeof(float) * (size_t)R * XL * YL);
+    float *ext = (float *)malloc(sizeof(float) * (size_t)XE * YE);
+    /* halo queues: what each rank's Write sent in the previous timestep */
+    float *snd_top = (float *)malloc(sizeof(float) * (size_t)R * YL);
+    float *snd_bot = (float *)malloc(sizeof(float) * (size_t)R * YL);
+    float *snd_lft = (float *)malloc(sizeof(float) * (size_t)R * XL);
+    float *snd_rgt = (float *)malloc(sizeof(float) * (size_t)R * XL);
+    if (!tile || !next || !ext || !snd_top || !snd_bot || !snd_lft || !snd_rgt) {
+        free(tile); free(next); free(ext); free(snd_top); free(snd_bot);
+        free(snd_lft); free(snd_rgt);
+        return -2;
+    }
+    /* SplitMemory */
+    for (int px = 0; px < PX; ++px)
+        for (int py = 0; py < PY; ++py)
+            for (int x = 0; x < XL; ++x)
+                memcpy(tile + ((size_t)(px * PY + py) * XL + x) * YL,
+                       in + ((size_t)px * XL + x) * Y + (size_t)py * YL,
+                       sizeof(float) * (size_t)YL);
+
+    for (int t = 0; t <= T; ++t) {          /* T+1 passes: t=0 is artificial */
+        for (int r = 0; r < R; ++r) {
+            const int ipx = r / PY, ipy = r % PY;
+            const float *my = tile + (size_t)r * XL * YL;
+            float *dst = next + (size_t)r * XL * YL;
+            /* Read: build the extended tile. */
+            for (size_t k = 0; k < (size_t)XE * YE; ++k) ext[k] = -100.0f;
+            for (int x = 0; x < XL; ++x)
+                memcpy(ext + (size_t)(x + 1) * YE + 1, my + (size_t)x * YL,
+                       sizeof(float) * (size_t)YL);
+            if (t > 0) {
+                /* receive_top <- rank above's bottom row (its send_bottom) */
+                if (ipx > 0) {
+                    const float *h = snd_bot + (size_t)((ipx - 1) * PY + ipy) * YL;
+                    memcpy(ext + 1, h, sizeof(float) * (size_t)YL);
+                }
+                if (ipx < PX - 1) {
+                    const float *h = snd_top + (size_t)((ipx + 1) * PY + ipy) * YL;
+                    memcpy(ext + (size_t)(XE - 1) * YE + 1, h, sizeof(float) * (size_t)YL);
+                }
+                if (ipy > 0) {
+                    const float *h = snd_rgt + (size_t)(ipx * PY + ipy - 1) * XL;
+                    for (int x = 0; x < XL; ++x) ext[(size_t)(x + 1) * YE] = h[x];
+                }
+                if (ipy < PY - 1) {
+                    const float *h = snd_lft + (size_t)(ipx * PY + ipy + 1) * XL;
+                    for (int x = 0; x < XL; ++x) ext[(size_t)(x + 1) * YE + YE - 1] = h[x];
+                }
+            }
+            /* Stencil */
+            for (int x = 0; x < XL; ++x) {
+                const float *n = ext + (size_t)x * YE;
+                const float *c = n + YE;
+                const float *s = c + YE;
+                for (int y = 0; y < YL; ++y) {
+                    const int gx_first = (ipx == 0 && x == 0);
+                    const int gx_last = (ipx == PX - 1 && x == XL - 1);
+                    const int gy_first = (ipy == 0 && y == 0);
+                    const int gy_last = (ipy == PY - 1 && y == YL - 1);
+                    float v;
+                    if (gx_first || gx_last || gy_first || gy_last || t == 0)
+                        v = c[y + 1];
+                    else
+                        v = cell_device(s[y + 1], c[y], c[y + 2], n[y + 1]);
+                    dst[(size_t)x * YL + y] = v;
+                }
+            }
+        }
+        /* Write: tee the halos of this pass (consumed at t+1 if t < T). */
+        for (int r = 0; r < R; ++r) {
+            const float *d = next + (size_t)r * XL * YL;
+            memcpy(snd_top + (size_t)r * YL, d, sizeof(float) * (size_t)YL);
+            memcpy(snd_bot + (size_t)r * YL, d + (size_t)(XL - 1) * YL,
+                   sizeof(float) * (size_t)YL);
+            for (int x = 0; x < XL; ++x) {
+                snd_lft[(size_t)r * XL + x] = d[(size_t)x * YL];
+                snd_rgt[(size_t)r * XL + x] = d[(size_t)x * YL + YL - 1];
+            }
+        }
+        float *tmp = tile; tile = next; next = tmp;
+    }
+    /* CombineMemory */
+    for (int px = 0; px < PX; ++px)
+        for (int py = 0; py < PY; ++py)
+            for (int x = 0; x < XL; ++x)
+                memcpy(out + ((size_t)px * XL + x) * Y + (size_t)py * YL,
+                       tile + ((size_t)(px * PY + py) * XL + x) * YL,
+                       sizeof(float) * (size_t)YL);
+    free(tile); free(next); free(ext);
+    free(snd_top); free(snd_bot); free(snd_lft); free(snd_rgt);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Reduce                                                                    */
+/* ------------------------------------------------------------------------ */
+
+/* Per-element fold of the root-side support kernel
+ * codegen/templates/reduce.cl:42-148 with SHIFT_REG / init from
+ * codegen/ops.py:110-141:
+ *   queue q[0..S-1] starts at init; contribution d (in arrival order):
+ *     q[S] = op(d, q[0]); shift q[j] = q[j+1]           (reduce.cl:65-69,100-105)
+ *   result = op(...op(op(init, q[0]), q[1])..., q[S-1])  (reduce.cl:120-125)
+ * op(A,B) = A+B, A>B?A:B, A<B?A:B       include/smi/reduce_operations.h:4-6
+ * Integer types wrap (two's complement), as the hardware adders do.
+ * contribs: nranks rows of `count` elements, row r = rank r's send buffer.
+ * arrival: permutation of ranks (NULL = rank order 0..n-1). */
+#define FOLD_BODY(T, S, INIT, OPEXPR)                                          \
+    do {                                                                       \
+        const T *src = (const T *)contribs;                                    \
+        T *dst = (T *)out;                                                     \
+        for (long i = 0; i < count; ++i) {                                     \
+            T q[(S) + 1];                                                      \
+            for (int j = 0; j <= (S); ++j) q[j] = (INIT);                      \
+            for (int k = 0; k < nranks; ++k) {                                 \
+                const int r = arrival ? arrival[k] : k;                        \
+                T A = src[(size_t)r * count + i], B = q[0];                    \
+                q[(S)] = (T)(OPEXPR);                                          \
+                for (int j = 0; j < (S); ++j) q[j] = q[j + 1];                 \
+            }                                                                  \
+            T res = (INIT);                                                    \
+            for (int j = 0; j < (S); ++j) {                                    \
+                T A = res, B = q[j];                                           \
+                res = (T)(OPEXPR);                                             \
+            }                                                                  \
+            dst[i] = res;                                                      \
+        }                                                                      \
+    } while (0)
+
+#define ADD_EXPR(A, B) ((A) + (B))
+#define MAX_EXPR(A, B) (((A) > (B)) ? (A) : (B))
+#define MIN_EXPR(A, B) (((A) < (B)) ? (A) : (B))
+
+/* wrapping integer add */
+#define IADD(T, UT) ((T)(UT)((UT)(A) + (UT)(B)))
+
+int oracle_reduce(const void *contribs, void *out, int nranks, long count,
+                  int dtype, int op, const int *arrival) {
+    if (nranks <= 0 || count < 0) return -1;
+    switch (dtype) {
+    case OR_FLOAT:
+        if (op == OR_ADD) FOLD_BODY(float, 4, 0.0f, ADD_EXPR(A, B));
+        else if (op == OR_MAX) FOLD_BODY(float, 4, FLT_MIN, MAX_EXPR(A, B));
+        else if (op == OR_MIN) FOLD_BODY(float, 4, FLT_MAX, MIN_EXPR(A, B));
+        else return -3;
+        return 0;
+    case OR_DOUBLE:
+        if (op == OR_ADD) FOLD_BODY(double, 4, 0.0, ADD_EXPR(A, B));
+        else if (op == OR_MAX) FOLD_BODY(double, 4, DBL_MIN, MAX_EXPR(A, B));
+        else if (op == OR_MIN) FOLD_BODY(double, 4, DBL_MAX, MIN_EXPR(A, B));
+        else return -3;
+        return 0;
+    case OR_INT:
+        if (op == OR_ADD) FOLD_BODY(int32_t, 1, 0, IADD(int32_t, uint32_t));
+        else if (op == OR_MAX) FOLD_BODY(int32_t, 1, INT_MIN, MAX_EXPR(A, B));
+        else if (op == OR_MIN) FOLD_BODY(int32_t, 1, INT_MAX, MIN_EXPR(A, B));
+        else return -3;
+        return 0;
+    case OR_SHORT:
+        if (op == OR_ADD) FOLD_BODY(int16_t, 1, 0, IADD(int16_t, uint16_t));
+        else if (op == OR_MAX) FOLD_BODY(int16_t, 1, SHRT_MIN, MAX_EXPR(A, B));
+        else if (op == OR_MIN) FOLD_BODY(int16_t, 1, SHRT_MAX, MIN_EXPR(A, B));
+        else return -3;
+        return 0;
+    case OR_CHAR:
+        if (op == OR_ADD) FOLD_BODY(int8_t, 1, 0, IADD(int8_t, uint8_t));
+        else if (op == OR_MAX) FOLD_BODY(int8_t, 1, CHAR_MIN, MAX_EXPR(A, B));
+        else if (op == OR_MIN) FOLD_BODY(int8_t, 1, CHAR_MAX, MIN_EXPR(A, B));
+        else return -3;
+        return 0;
+    default:
+        return -2;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* gesummv                                                                   */
+/* ------------------------------------------------------------------------ */
+
+/* Row-streamed GEMV fold of examples/kernels/gesummv_rank0.cl:53-181
+ * (row_streamed=1, W=64, TILE_M=128, single precision branch):
+ *   c_k  = ((0 + a[64k]*x[64k]) + a[64k+1]*x[64k+1]) + ...      (:137-149)
+ *   per 128-column tile t: acc_o = (0 + alpha*c_{2t}) + alpha*c_{2t+1} (:111,158)
+ *   y = ((0 + acc_o(0)) + acc_o(1)) + ...       prev = local_y[i] (:126-127,171)
+ * M must be a multiple of 64 (gesummv_rank0.cl:268).  When M is an odd
+ * multiple of 64 the final tile's second chunk reads zero-padded x
+ * (READ_VECTOR_X, gesummv_rank0.cl:219-222) and contributes c = +0. */
+static float gemv_row(const float *a, const float *x, int M, float alpha) {
+    const int chunks = M / 64;
+    float y = 0.0f;
+    for (int t = 0; t < (chunks + 1) / 2; ++t) {
+        float acc_o = 0.0f;
+        for (int jj = 0; jj < 2; ++jj) {
+            const int k = 2 * t + jj;
+            float acc_i = 0.0f;
+            if (k < chunks) {
+                for (int j = 0; j < 64; ++j) {
+                    float p = a[64 * k + j] * x[64 * k + j];
+                    acc_i = acc_i + p;
+                }
+            }
+            float q = alpha * acc_i;
+            acc_o = acc_o + q;
+        }
+        y = y + acc_o;
+    }
+    return y;
+}
+
+/* y_i = gemv_row(A_i, alpha) + gemv_row(B_i, beta): rank 0 runs gemv with
+ * alpha (gesummv_smi.cpp:224), rank 1 with beta as its alpha (:248), and
+ * axpy adds rank0 + rank1 (gesummv_rank0.cl:199). */
+int oracle_gesummv(const float *A, const float *B, const float *x, float *y,
+                   int N, int M, float alpha, float beta, int threads) {
+    if (N < 0 || M < 0 || M % 64) return -1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < N; ++i) {
+        float r0 = gemv_row(A + (size_t)i * M, x, M, alpha);
+        float r1 = gemv_row(B + (size_t)i * M, x, M, beta);
+        y[i] = r0 + r1;
+    }
+    return 0;
+}
+
+int oracle_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

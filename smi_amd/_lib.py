@@ -1,0 +1,112 @@
+"""ctypes binding of libsmi_amd.so (the C ABI of include/smi/*.h).
+
+torch is imported first on purpose: its wheel ships its own HIP runtime
+(libamdhip64.so.7) and RCCL (librccl.so.1); loading them before our library
+makes the dynamic linker resolve our library's dependencies to those same
+copies, so device pointers, streams and events are shared with torch.
+
+There is no fallback: if the library is missing or fails to load, every
+entry point raises.  The product path never touches the CPU oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (see module docstring)
+
+from . import build as _build
+
+_lib = None
+
+SMI_SUCCESS = 0
+SMI_UNIQUE_ID_BYTES = 128
+
+# include/smi/data_types.h (same values as the reference's data_types.h:10-16)
+SMI_INT, SMI_FLOAT, SMI_DOUBLE, SMI_CHAR, SMI_SHORT = 1, 2, 3, 4, 5
+# include/smi/reduce.h (reference reduce.h:18-22)
+SMI_ADD, SMI_MAX, SMI_MIN = 0, 1, 2
+# include/smi/stencil.h
+SIDE_COPY, SIDE_HALO, SIDE_SKIP = 0, 1, 2
+# include/smi/profiling.h
+PROF_STENCIL_SWEEP, PROF_STENCIL_EDGE, PROF_REDUCE_FOLD, PROF_GEMV = 0, 1, 2, 3
+
+
+class SMIError(RuntimeError):
+    pass
+
+
+class SMI_Comm(ctypes.Structure):
+    _fields_ = [("rank", ctypes.c_int), ("size", ctypes.c_int), ("handle", ctypes.c_int)]
+
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+SZ = ctypes.c_size_t
+F = ctypes.c_float
+
+# name -> (restype, argtypes); every symbol declared in include/smi/*.h
+SIGNATURES = {
+    "smi_last_error": (ctypes.c_char_p, []),
+    "smi_get_unique_id": (I, [P, I]),
+    "smi_init": (I, [I, I, I, P, I, ctypes.POINTER(SMI_Comm)]),
+    "smi_local_group_create": (I, [I, ctypes.POINTER(I)]),
+    "smi_init_local": (I, [I, I, I, ctypes.POINTER(SMI_Comm)]),
+    "smi_finalize": (I, [SMI_Comm]),
+    "smi_device_count": (I, [ctypes.POINTER(I)]),
+    "smi_stream_synchronize": (I, [P]),
+    "smi_stencil_step": (I, [P, P, I, I, ctypes.POINTER(I), ctypes.POINTER(P), P, P, P]),
+    "smi_stencil_run": (I, [SMI_Comm, P, P, I, I, I, I, I, P, ctypes.POINTER(I)]),
+    "smi_stencil_set_tuning": (I, [I, I, I, I]),
+    "smi_stencil_get_tuning": (I, [ctypes.POINTER(I)] * 4),
+    "smi_reduce": (I, [SMI_Comm, P, P, SZ, I, I, I, I, P]),
+    "smi_reduce_fold": (I, [P, P, I, SZ, SZ, I, I, P]),
+    "smi_bcast": (I, [SMI_Comm, P, SZ, I, I, I, P]),
+    "smi_type_size": (SZ, [I]),
+    "smi_gemv_rows": (I, [P, P, P, P, I, I, I, F, F, P]),
+    "smi_gesummv": (I, [SMI_Comm, P, P, P, P, I, I, F, F, I, P]),
+    "smi_prof_enable": (I, [I]),
+    "smi_prof_reset": (I, []),
+    "smi_prof_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),
+}
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load(build_if_missing: bool = True) -> ctypes.CDLL:
+    """Load (building first if needed and allowed) libsmi_amd.so."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path) or (build_if_missing and _build._stale()):
+        if not build_if_missing:
+            raise SMIError(f"{path} missing: run smi_amd.build.build()")
+        _build.build()
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != SMI_SUCCESS:
+        msg = load().smi_last_error()
+        msg = msg.decode(errors="replace") if msg else ""
+        raise SMIError(f"{what} failed with code {rc}: {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)
+
+
+def stream_handle(stream=None) -> int:
+    """hipStream_t of a torch stream (default: torch's current stream)."""
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream)

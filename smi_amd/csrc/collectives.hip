@@ -1,0 +1,312 @@
+// collectives.hip -- SMI_Reduce and SMI_Bcast on whole device buffers.
+//
+// Reference replaced (ryutakashino/SMI):
+//   SMI_Reduce + smi_kernel_reduce_<p>   codegen/templates/reduce.cl:3-245
+//     root-gathering reduce, one element per 32-B packet, 16-deep credit
+//     window, per-slot rotating fold (SHIFT_REG, codegen/ops.py:110-141)
+//   SMI_Bcast + smi_kernel_bcast_<p>     codegen/templates/bcast.cl:3-149
+//     root packs 7 elements per packet, linear fan-out to every rank
+// MI355X design: on a fully connected xGMI node the root's links are the
+// bottleneck of a rooted collective, so both are split over all ranks:
+//   reduce = owner-chunk exchange (rank r sends chunk c of its buffer to
+//            owner c) -> canonical rank-order fold on each owner (HIP kernel,
+//            bit-identical to the reference fold with arrival = rank order)
+//            -> owners send their reduced chunk to the root;
+//   bcast  = scatter of the root's chunks -> all-gather between the ranks
+//            (small messages: direct fan-out from the root).
+// Every step is a transport group of point-to-point transfers on the
+// caller's stream (RCCL over xGMI in production).
+#include <algorithm>
+
+#include "smi_internal.h"
+
+namespace smi {
+
+constexpr int kMaxFoldRanks = 64;
+
+struct FoldRows {
+    const void *row[kMaxFoldRanks];
+};
+
+template <typename T, int OP>
+__device__ __forceinline__ T op_apply(T a, T b) {
+    if constexpr (OP == SMI_ADD) {
+        if constexpr (std::is_same<T, float>::value) return __fadd_rn(a, b);
+        else if constexpr (std::is_same<T, double>::value) return __dadd_rn(a, b);
+        else {
+            using U = typename std::make_unsigned<T>::type;  // wrapping add
+            return (T)(U)((U)a + (U)b);
+        }
+    } else if constexpr (OP == SMI_MAX) {
+        return a > b ? a : b;   // SMI_OP_MAX, include/smi/reduce_operations.h:6
+    } else {
+        return a < b ? a : b;   // SMI_OP_MIN, include/smi/reduce_operations.h:5
+    }
+}
+
+// codegen/ops.py:124-141 SHIFT_REG_INIT (note FLT_MIN / DBL_MIN, the
+// smallest positive normals, for MAX -- kept as the reference has it).
+template <typename T, int OP>
+__device__ __forceinline__ T op_init() {
+    if constexpr (OP == SMI_ADD) return (T)0;
+    else if constexpr (OP == SMI_MAX) {
+        if constexpr (std::is_same<T, float>::value) return 1.17549435e-38f;
+        else if constexpr (std::is_same<T, double>::value) return 2.2250738585072014e-308;
+        else return std::numeric_limits<T>::min();
+    } else {
+        if constexpr (std::is_same<T, float>::value) return 3.40282347e+38f;
+        else if constexpr (std::is_same<T, double>::value) return 1.7976931348623157e+308;
+        else return std::numeric_limits<T>::max();
+    }
+}
+
+// Fold of reduce.cl:65-69,100-105,120-125 for one element, contributions in
+// rank order, S slots (4 for float/double, 1 for the integer types).
+// Each thread folds VEC consecutive elements loaded 16 bytes per row.
+template <typename T, int S, int OP>
+__global__ __launch_bounds__(256) void fold_kernel(FoldRows rows, T *__restrict__ out, int n,
+                                                   size_t count, int vec_ok) {
+    constexpr int VEC = 16 / sizeof(T);
+    const size_t nvec = count / VEC;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < (count + VEC - 1) / VEC; v += stride) {
+        const size_t base = v * VEC;
+        const bool full = vec_ok && v < nvec;
+        T q[VEC][S];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e)
+#pragma unroll
+            for (int j = 0; j < S; ++j) q[e][j] = op_init<T, OP>();
+        for (int k = 0; k < n; ++k) {
+            const T *src = (const T *)rows.row[k] + base;
+            T d[VEC];
+            if (full) {
+                *reinterpret_cast<uint4 *>(d) = *reinterpret_cast<const uint4 *>(src);
+            } else {
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) d[e] = (base + e < count) ? src[e] : T(0);
+            }
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                const T nv = op_apply<T, OP>(d[e], q[e][0]);
+#pragma unroll
+                for (int j = 0; j < S - 1; ++j) q[e][j] = q[e][j + 1];
+                q[e][S - 1] = nv;
+            }
+        }
+        T r[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+            T res = op_init<T, OP>();
+#pragma unroll
+            for (int j = 0; j < S; ++j) res = op_apply<T, OP>(res, q[e][j]);
+            r[e] = res;
+        }
+        if (full) {
+            *reinterpret_cast<uint4 *>(out + base) = *reinterpret_cast<const uint4 *>(r);
+        } else {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e)
+                if (base + e < count) out[base + e] = r[e];
+        }
+    }
+}
+
+template <typename T, int S, int OP>
+static void launch_fold_t(const FoldRows &rows, void *out, int n, size_t count, int vec_ok,
+                          hipStream_t s) {
+    constexpr int VEC = 16 / sizeof(T);
+    const size_t work = (count + VEC - 1) / VEC;
+    const int blocks = (int)std::max<size_t>(1, std::min<size_t>((work + 255) / 256, 4096));
+    hipLaunchKernelGGL((fold_kernel<T, S, OP>), dim3(blocks), dim3(256), 0, s, rows, (T *)out, n, count,
+                       vec_ok);
+}
+
+template <typename T, int S>
+static int launch_fold_op(const FoldRows &rows, void *out, int n, size_t count, int vec_ok, int op,
+                          hipStream_t s) {
+    switch (op) {
+    case SMI_ADD: launch_fold_t<T, S, SMI_ADD>(rows, out, n, count, vec_ok, s); break;
+    case SMI_MAX: launch_fold_t<T, S, SMI_MAX>(rows, out, n, count, vec_ok, s); break;
+    case SMI_MIN: launch_fold_t<T, S, SMI_MIN>(rows, out, n, count, vec_ok, s); break;
+    default: set_error("unsupported reduce op"); return SMI_ERR_UNSUPPORTED;
+    }
+    return SMI_SUCCESS;
+}
+
+static int launch_fold(const FoldRows &rows, void *out, int n, size_t count, int type, int op,
+                       hipStream_t s) {
+    SMI_ARG_CHECK(n >= 1 && n <= kMaxFoldRanks, "fold supports 1..64 contributions");
+    if (count == 0) return SMI_SUCCESS;
+    int vec_ok = ((uintptr_t)out & 15u) == 0;
+    for (int k = 0; k < n; ++k) vec_ok &= ((uintptr_t)rows.row[k] & 15u) == 0;
+    int tok = -1;
+    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_REDUCE_FOLD, s, &tok));
+    int rc;
+    switch (type) {  // SHIFT_REG: codegen/ops.py:110-116
+    case SMI_FLOAT: rc = launch_fold_op<float, 4>(rows, out, n, count, vec_ok, op, s); break;
+    case SMI_DOUBLE: rc = launch_fold_op<double, 4>(rows, out, n, count, vec_ok, op, s); break;
+    case SMI_INT: rc = launch_fold_op<int32_t, 1>(rows, out, n, count, vec_ok, op, s); break;
+    case SMI_SHORT: rc = launch_fold_op<int16_t, 1>(rows, out, n, count, vec_ok, op, s); break;
+    case SMI_CHAR: rc = launch_fold_op<int8_t, 1>(rows, out, n, count, vec_ok, op, s); break;
+    default: set_error("unsupported data type"); return SMI_ERR_UNSUPPORTED;
+    }
+    SMI_TRY(rc);
+    SMI_HIP_CHECK(hipGetLastError());
+    if (tok >= 0) SMI_TRY(prof_end(tok, s));
+    return SMI_SUCCESS;
+}
+
+// Owner chunk c covers elements [c*cs, min((c+1)*cs, count)); cs is a
+// multiple of 16 bytes so every chunk of an aligned buffer stays aligned.
+static size_t chunk_elems(size_t count, int n, size_t esz) {
+    const size_t per16 = 16 / std::min<size_t>(16, esz);
+    size_t cs = (count + n - 1) / n;
+    cs = (cs + per16 - 1) / per16 * per16;
+    return std::max<size_t>(cs, per16);
+}
+static size_t chunk_len(size_t count, size_t cs, int c) {
+    const size_t b = (size_t)c * cs;
+    return b >= count ? 0 : std::min(cs, count - b);
+}
+
+}  // namespace smi
+
+using namespace smi;
+
+extern "C" {
+
+int smi_reduce_fold(const void *contribs, void *out, int nranks, size_t count, size_t ld,
+                    SMI_Datatype type, SMI_Op op, SMI_Stream stream) {
+    SMI_ARG_CHECK(out && (contribs || count == 0), "NULL buffer");
+    SMI_ARG_CHECK(nranks >= 1 && nranks <= kMaxFoldRanks, "nranks out of range");
+    SMI_ARG_CHECK(ld >= count, "ld < count");
+    const size_t esz = type_size(type);
+    if (esz == 0) {
+        set_error("unsupported data type");
+        return SMI_ERR_UNSUPPORTED;
+    }
+    FoldRows rows{};
+    for (int k = 0; k < nranks; ++k) rows.row[k] = (const char *)contribs + (size_t)k * ld * esz;
+    return launch_fold(rows, out, nranks, count, type, op, (hipStream_t)stream);
+}
+
+int smi_reduce(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count, SMI_Datatype type,
+               SMI_Op op, int root, int port, SMI_Stream stream_) {
+    (void)port;  // ports only order operations in the reference; one stream orders them here
+    Comm *c = lookup_comm(comm);
+    if (!c) {
+        set_error("unknown communicator");
+        return SMI_ERR_BAD_COMM;
+    }
+    const int n = c->size, me = c->rank;
+    SMI_ARG_CHECK(root >= 0 && root < n, "root out of range");
+    SMI_ARG_CHECK(n <= kMaxFoldRanks, "reduce supports up to 64 ranks");
+    SMI_ARG_CHECK(op >= SMI_ADD && op <= SMI_MIN, "bad op");
+    const size_t esz = type_size(type);
+    if (esz == 0) {
+        set_error("unsupported data type");
+        return SMI_ERR_UNSUPPORTED;
+    }
+    if (count == 0) return SMI_SUCCESS;
+    SMI_ARG_CHECK(sendbuf, "NULL sendbuf");
+    SMI_ARG_CHECK(me != root || recvbuf, "NULL recvbuf on root");
+    hipStream_t s = (hipStream_t)stream_;
+
+    if (n == 1) {
+        FoldRows rows{};
+        rows.row[0] = sendbuf;
+        return launch_fold(rows, recvbuf, 1, count, type, op, s);
+    }
+    const size_t cs = chunk_elems(count, n, esz);
+    const size_t my_len = chunk_len(count, cs, me);
+    // workspace: n staging rows of cs elements (+ one result chunk off-root)
+    void *ws = nullptr;
+    SMI_TRY(comm_workspace(c, (size_t)(n + 1) * cs * esz, &ws));
+    char *stage = (char *)ws;
+    char *mine = stage + (size_t)n * cs * esz;
+    const char *sb = (const char *)sendbuf;
+    Transport *tp = c->transport.get();
+
+    // 1. owner-chunk exchange: chunk k of my buffer -> owner k
+    SMI_TRY(tp->begin(s));
+    for (int k = 0; k < n; ++k) {
+        if (k == me) continue;
+        SMI_TRY(tp->send(sb + (size_t)k * cs * esz, chunk_len(count, cs, k) * esz, k));
+        SMI_TRY(tp->recv(stage + (size_t)k * cs * esz, my_len * esz, k));
+    }
+    SMI_TRY(tp->end());
+    // 2. canonical rank-order fold of my chunk
+    char *dst = (me == root) ? (char *)recvbuf + (size_t)me * cs * esz : mine;
+    if (my_len) {
+        FoldRows rows{};
+        for (int k = 0; k < n; ++k)
+            rows.row[k] = (k == me) ? (const void *)(sb + (size_t)me * cs * esz)
+                                    : (const void *)(stage + (size_t)k * cs * esz);
+        SMI_TRY(launch_fold(rows, dst, n, my_len, type, op, s));
+    }
+    // 3. gather the reduced chunks on the root
+    SMI_TRY(tp->begin(s));
+    if (me == root) {
+        for (int k = 0; k < n; ++k)
+            if (k != root)
+                SMI_TRY(tp->recv((char *)recvbuf + (size_t)k * cs * esz, chunk_len(count, cs, k) * esz, k));
+    } else {
+        SMI_TRY(tp->send(mine, my_len * esz, root));
+    }
+    return tp->end();
+}
+
+int smi_bcast(SMI_Comm comm, void *buf, size_t count, SMI_Datatype type, int root, int port,
+              SMI_Stream stream_) {
+    (void)port;
+    Comm *c = lookup_comm(comm);
+    if (!c) {
+        set_error("unknown communicator");
+        return SMI_ERR_BAD_COMM;
+    }
+    const int n = c->size, me = c->rank;
+    SMI_ARG_CHECK(root >= 0 && root < n, "root out of range");
+    const size_t esz = type_size(type);
+    if (esz == 0) {
+        set_error("unsupported data type");
+        return SMI_ERR_UNSUPPORTED;
+    }
+    if (count == 0 || n == 1) return SMI_SUCCESS;
+    SMI_ARG_CHECK(buf, "NULL buffer");
+    hipStream_t s = (hipStream_t)stream_;
+    Transport *tp = c->transport.get();
+    char *b = (char *)buf;
+    const size_t bytes = count * esz;
+
+    if (bytes <= (size_t)256 * 1024 || n == 2) {  // latency-bound: direct fan-out
+        SMI_TRY(tp->begin(s));
+        if (me == root) {
+            for (int k = 0; k < n; ++k)
+                if (k != root) SMI_TRY(tp->send(b, bytes, k));
+        } else {
+            SMI_TRY(tp->recv(b, bytes, root));
+        }
+        return tp->end();
+    }
+    // scatter: the root's chunk k -> rank k (into its own position)
+    const size_t cs = chunk_elems(count, n, esz);
+    SMI_TRY(tp->begin(s));
+    if (me == root) {
+        for (int k = 0; k < n; ++k)
+            if (k != root) SMI_TRY(tp->send(b + (size_t)k * cs * esz, chunk_len(count, cs, k) * esz, k));
+    } else {
+        SMI_TRY(tp->recv(b + (size_t)me * cs * esz, chunk_len(count, cs, me) * esz, root));
+    }
+    SMI_TRY(tp->end());
+    // all-gather among the ranks; the root only sends its own chunk
+    SMI_TRY(tp->begin(s));
+    for (int k = 0; k < n; ++k) {
+        if (k == me) continue;
+        if (k != root) SMI_TRY(tp->send(b + (size_t)me * cs * esz, chunk_len(count, cs, me) * esz, k));
+        if (me != root) SMI_TRY(tp->recv(b + (size_t)k * cs * esz, chunk_len(count, cs, k) * esz, k));
+    }
+    return tp->end();
+}
+
+}  // extern "C"

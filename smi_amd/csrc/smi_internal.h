@@ -1,0 +1,94 @@
+// smi_internal.h -- shared internals of libsmi_amd.so (not installed).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "smi.h"
+
+namespace smi {
+
+// ---------------------------------------------------------------- errors --
+void set_error(const std::string &msg);
+
+#define SMI_HIP_CHECK(expr)                                                    \
+    do {                                                                       \
+        hipError_t _e = (expr);                                                \
+        if (_e != hipSuccess) {                                                \
+            ::smi::set_error(std::string(#expr) + ": " + hipGetErrorString(_e) \
+                             + " (" + __FILE__ + ":" + std::to_string(__LINE__) \
+                             + ")");                                           \
+            return SMI_ERR_HIP;                                                \
+        }                                                                      \
+    } while (0)
+
+#define SMI_ARG_CHECK(cond, msg)                                               \
+    do {                                                                       \
+        if (!(cond)) {                                                         \
+            ::smi::set_error(std::string("invalid argument: ") + (msg));       \
+            return SMI_ERR_INVALID_ARG;                                        \
+        }                                                                      \
+    } while (0)
+
+#define SMI_TRY(expr)                                                          \
+    do {                                                                       \
+        int _rc = (expr);                                                      \
+        if (_rc != SMI_SUCCESS) return _rc;                                    \
+    } while (0)
+
+// ------------------------------------------------------------- transport --
+// Point-to-point byte transport between the ranks of one communicator.
+// Usage mirrors an RCCL group: begin(stream); send/recv ...; end().  All ops
+// of a group are ordered after the work already queued on `stream`, and work
+// queued on `stream` after end() observes every receive of the group and may
+// overwrite every send buffer of the group.
+class Transport {
+  public:
+    virtual ~Transport() = default;
+    virtual int begin(hipStream_t stream) = 0;
+    virtual int send(const void *buf, size_t bytes, int peer) = 0;
+    virtual int recv(void *buf, size_t bytes, int peer) = 0;
+    virtual int end() = 0;
+};
+
+std::unique_ptr<Transport> make_rccl_transport(int rank, int size,
+                                               const void *unique_id,
+                                               int id_bytes, int *rc);
+std::unique_ptr<Transport> make_local_transport(int group_id, int rank,
+                                                int *rc);
+int local_group_size(int group_id);
+
+// ------------------------------------------------------------ communicator --
+struct Comm {
+    int rank = 0;
+    int size = 1;
+    int device = 0;
+    std::unique_ptr<Transport> transport;
+    hipStream_t comm_stream = nullptr;  // dedicated halo / collective stream
+    // device workspace (grown on demand, never shrunk)
+    void *work = nullptr;
+    size_t work_bytes = 0;
+    // halo staging for the stencil: [top, bottom, left, right] in + send L/R
+    float *halo = nullptr;
+    size_t halo_elems = 0;
+    std::vector<hipEvent_t> events;  // reusable sync events
+};
+
+Comm *lookup_comm(SMI_Comm c);
+int comm_workspace(Comm *c, size_t bytes, void **ptr);
+int comm_event(Comm *c, int idx, hipEvent_t *ev);
+
+// ------------------------------------------------------------ profiling --
+bool prof_enabled();
+// Bracket one launch: call before (returns a token) and after the launch.
+int prof_begin(int kernel, hipStream_t stream, int *token);
+int prof_end(int token, hipStream_t stream);
+
+size_t type_size(int type);
+
+}  // namespace smi

@@ -1,0 +1,265 @@
+// transport.cpp -- the two point-to-point transports behind the channels.
+//
+// The reference moves 32-byte packets through CK_S/CK_R kernels and QSFP
+// links chosen by routing tables (codegen/templates/cks.cl:3-84, ckr.cl:
+// 3-88); on one MI355X node every GPU pair is a direct xGMI link, so a
+// transfer is a plain RCCL send/recv between the two ranks.
+//
+//  * RcclTransport  -- production: one process per GPU, RCCL over xGMI.
+//  * LocalTransport -- ranks are host threads of one process sharing one (or
+//    several) devices; a transfer is a device-to-device hipMemcpyAsync
+//    ordered by HIP events.  It exists so that multi-rank parity tests can run
+//    on a single GPU (RCCL refuses two ranks on one device).
+#include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+
+#include "smi_internal.h"
+
+namespace smi {
+
+// ================================================================= RCCL ==
+class RcclTransport final : public Transport {
+  public:
+    explicit RcclTransport(ncclComm_t c) : comm_(c) {}
+    ~RcclTransport() override {
+        if (comm_) ncclCommDestroy(comm_);
+    }
+    int begin(hipStream_t stream) override {
+        stream_ = stream;
+        return check(ncclGroupStart(), "ncclGroupStart");
+    }
+    int send(const void *buf, size_t bytes, int peer) override {
+        if (bytes == 0) return SMI_SUCCESS;
+        return check(ncclSend(buf, bytes, ncclUint8, peer, comm_, stream_), "ncclSend");
+    }
+    int recv(void *buf, size_t bytes, int peer) override {
+        if (bytes == 0) return SMI_SUCCESS;
+        return check(ncclRecv(buf, bytes, ncclUint8, peer, comm_, stream_), "ncclRecv");
+    }
+    int end() override { return check(ncclGroupEnd(), "ncclGroupEnd"); }
+
+    static int check(ncclResult_t r, const char *what) {
+        if (r == ncclSuccess) return SMI_SUCCESS;
+        set_error(std::string(what) + ": " + ncclGetErrorString(r));
+        return SMI_ERR_COMM;
+    }
+
+  private:
+    ncclComm_t comm_ = nullptr;
+    hipStream_t stream_ = nullptr;
+};
+
+std::unique_ptr<Transport> make_rccl_transport(int rank, int size,
+                                               const void *unique_id,
+                                               int id_bytes, int *rc) {
+    if (id_bytes < (int)sizeof(ncclUniqueId)) {
+        set_error("unique id too short");
+        *rc = SMI_ERR_INVALID_ARG;
+        return nullptr;
+    }
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof(id));
+    ncclComm_t comm = nullptr;
+    *rc = RcclTransport::check(ncclCommInitRank(&comm, size, id, rank), "ncclCommInitRank");
+    if (*rc != SMI_SUCCESS) return nullptr;
+    return std::make_unique<RcclTransport>(comm);
+}
+
+// ================================================================ local ==
+namespace {
+
+struct Post {
+    const void *buf = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ready = nullptr;  // sender's stream reached the send
+    hipEvent_t done = nullptr;   // receiver's copy finished
+    bool copied = false;         // `done` has been recorded
+    int status = SMI_SUCCESS;
+};
+
+struct LocalGroup {
+    int size = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<std::pair<int, int>, std::deque<std::shared_ptr<Post>>> mailbox;
+    int joined = 0;
+};
+
+std::mutex g_groups_mu;
+std::map<int, std::shared_ptr<LocalGroup>> g_groups;
+int g_next_group = 1;
+
+std::shared_ptr<LocalGroup> find_group(int id) {
+    std::lock_guard<std::mutex> lk(g_groups_mu);
+    auto it = g_groups.find(id);
+    return it == g_groups.end() ? nullptr : it->second;
+}
+
+}  // namespace
+
+int local_group_size(int group_id) {
+    auto g = find_group(group_id);
+    return g ? g->size : 0;
+}
+
+class LocalTransport final : public Transport {
+  public:
+    LocalTransport(std::shared_ptr<LocalGroup> g, int rank) : g_(std::move(g)), rank_(rank) {}
+
+    int begin(hipStream_t stream) override {
+        stream_ = stream;
+        sends_.clear();
+        recvs_.clear();
+        return SMI_SUCCESS;
+    }
+    int send(const void *buf, size_t bytes, int peer) override {
+        if (peer < 0 || peer >= g_->size) {
+            set_error("send: peer out of range");
+            return SMI_ERR_INVALID_ARG;
+        }
+        sends_.push_back({const_cast<void *>(buf), bytes, peer});
+        return SMI_SUCCESS;
+    }
+    int recv(void *buf, size_t bytes, int peer) override {
+        if (peer < 0 || peer >= g_->size) {
+            set_error("recv: peer out of range");
+            return SMI_ERR_INVALID_ARG;
+        }
+        recvs_.push_back({buf, bytes, peer});
+        return SMI_SUCCESS;
+    }
+
+    // Rendezvous: (1) post every send with a `ready` event on our stream;
+    // (2) for every receive, wait for the matching post (FIFO per
+    // (src, dst) pair, like the reference's per-port FIFO order), make our
+    // stream wait on its `ready`, copy, record `done`; (3) make our stream
+    // wait for the `done` of each of our sends, so later work may reuse the
+    // send buffers.
+    int end() override {
+        std::vector<std::shared_ptr<Post>> mine;
+        for (auto &s : sends_) {
+            auto p = std::make_shared<Post>();
+            p->buf = s.buf;
+            p->bytes = s.bytes;
+            SMI_HIP_CHECK(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
+            SMI_HIP_CHECK(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
+            SMI_HIP_CHECK(hipEventRecord(p->ready, stream_));
+            mine.push_back(p);
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_->mu);
+            for (size_t i = 0; i < sends_.size(); ++i)
+                g_->mailbox[{rank_, sends_[i].peer}].push_back(mine[i]);
+        }
+        g_->cv.notify_all();
+
+        int rc = SMI_SUCCESS;
+        for (auto &r : recvs_) {
+            std::shared_ptr<Post> p;
+            {
+                std::unique_lock<std::mutex> lk(g_->mu);
+                auto &q = g_->mailbox[{r.peer, rank_}];
+                g_->cv.wait(lk, [&] { return !q.empty(); });
+                p = q.front();
+                q.pop_front();
+            }
+            int st = SMI_SUCCESS;
+            if (p->bytes != r.bytes) {
+                set_error("local transport: send/recv size mismatch");
+                st = SMI_ERR_COMM;
+            } else {
+                if (hipStreamWaitEvent(stream_, p->ready, 0) != hipSuccess ||
+                    (r.bytes && hipMemcpyAsync(r.buf, p->buf, r.bytes, hipMemcpyDeviceToDevice,
+                                               stream_) != hipSuccess))
+                    st = SMI_ERR_HIP;
+            }
+            if (hipEventRecord(p->done, stream_) != hipSuccess && st == SMI_SUCCESS) st = SMI_ERR_HIP;
+            {
+                std::lock_guard<std::mutex> lk(g_->mu);
+                p->status = st;
+                p->copied = true;
+            }
+            g_->cv.notify_all();
+            if (st != SMI_SUCCESS && rc == SMI_SUCCESS) {
+                if (st == SMI_ERR_HIP) set_error("local transport: HIP copy failed");
+                rc = st;
+            }
+        }
+        for (auto &p : mine) {
+            {
+                std::unique_lock<std::mutex> lk(g_->mu);
+                g_->cv.wait(lk, [&] { return p->copied; });
+            }
+            if (p->status != SMI_SUCCESS && rc == SMI_SUCCESS) {
+                set_error("local transport: peer failed to receive");
+                rc = p->status;
+            }
+            SMI_HIP_CHECK(hipStreamWaitEvent(stream_, p->done, 0));
+            // destruction is deferred by the runtime until the events complete
+            SMI_HIP_CHECK(hipEventDestroy(p->ready));
+            SMI_HIP_CHECK(hipEventDestroy(p->done));
+        }
+        sends_.clear();
+        recvs_.clear();
+        return rc;
+    }
+
+  private:
+    struct Op {
+        void *buf;
+        size_t bytes;
+        int peer;
+    };
+    std::shared_ptr<LocalGroup> g_;
+    int rank_;
+    hipStream_t stream_ = nullptr;
+    std::vector<Op> sends_, recvs_;
+};
+
+std::unique_ptr<Transport> make_local_transport(int group_id, int rank, int *rc) {
+    auto g = find_group(group_id);
+    if (!g) {
+        set_error("unknown local group");
+        *rc = SMI_ERR_BAD_COMM;
+        return nullptr;
+    }
+    if (rank < 0 || rank >= g->size) {
+        set_error("rank out of range for local group");
+        *rc = SMI_ERR_INVALID_ARG;
+        return nullptr;
+    }
+    *rc = SMI_SUCCESS;
+    return std::make_unique<LocalTransport>(g, rank);
+}
+
+}  // namespace smi
+
+extern "C" {
+
+int smi_get_unique_id(void *id, int id_bytes) {
+    using namespace smi;
+    SMI_ARG_CHECK(id && id_bytes >= (int)sizeof(ncclUniqueId), "unique id buffer too small");
+    ncclUniqueId u;
+    SMI_TRY(RcclTransport::check(ncclGetUniqueId(&u), "ncclGetUniqueId"));
+    memcpy(id, &u, sizeof(u));
+    return SMI_SUCCESS;
+}
+
+int smi_local_group_create(int size, int *group_id) {
+    using namespace smi;
+    SMI_ARG_CHECK(group_id && size >= 1, "size/group_id");
+    auto g = std::make_shared<LocalGroup>();
+    g->size = size;
+    std::lock_guard<std::mutex> lk(g_groups_mu);
+    int id = g_next_group++;
+    g_groups[id] = g;
+    *group_id = id;
+    return SMI_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,97 @@
+"""Host mirror of the stencil_smi program (examples/host/stencil_smi.cpp).
+
+Same decomposition and naming as the reference host: the X x Y grid is split
+into PX x PY tiles, rank = i_px*PY + i_py owns rows [i_px*X_LOCAL, ..) and
+columns [i_py*Y_LOCAL, ..) (SplitMemory / CombineMemory,
+stencil_smi.cpp:48-62,80-93; rank map :133-134); the default test grid is 0
+in the interior and 1 on the four edges (:175-187).  Every sweep runs in the
+HIP kernels of libsmi_amd.so; device buffers are torch tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .comm import Comm
+
+BOUNDARY_VALUE = 1.0  # examples/include/stencil.h.in:8
+
+
+def init_grid(X: int, Y: int) -> np.ndarray:
+    """0 interior, BOUNDARY_VALUE on the four edges (stencil_smi.cpp:175-187)."""
+    g = np.zeros((X, Y), dtype=np.float32)
+    g[0, :] = BOUNDARY_VALUE
+    g[X - 1, :] = BOUNDARY_VALUE
+    g[:, 0] = BOUNDARY_VALUE
+    g[:, Y - 1] = BOUNDARY_VALUE
+    return g
+
+
+def split_memory(grid: np.ndarray, PX: int, PY: int) -> list[np.ndarray]:
+    """SplitMemory (stencil_smi.cpp:48-62): tile of rank px*PY+py."""
+    X, Y = grid.shape
+    if X % PX or Y % PY:
+        raise ValueError("grid not divisible by the process grid")
+    XL, YL = X // PX, Y // PY
+    return [np.ascontiguousarray(grid[px * XL:(px + 1) * XL, py * YL:(py + 1) * YL])
+            for px in range(PX) for py in range(PY)]
+
+
+def combine_memory(tiles: list[np.ndarray], PX: int, PY: int) -> np.ndarray:
+    """CombineMemory (stencil_smi.cpp:80-93)."""
+    XL, YL = tiles[0].shape
+    out = np.empty((PX * XL, PY * YL), dtype=np.float32)
+    for px in range(PX):
+        for py in range(PY):
+            out[px * XL:(px + 1) * XL, py * YL:(py + 1) * YL] = tiles[px * PY + py]
+    return out
+
+
+def rank_coords(rank: int, PY: int) -> tuple[int, int]:
+    """i_px = rank / PY, i_py = rank % PY (stencil_smi.cpp:133-134)."""
+    return rank // PY, rank % PY
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def step(inp: torch.Tensor, out: torch.Tensor, modes=(0, 0, 0, 0), halos=(None, None, None, None),
+         send_left: torch.Tensor | None = None, send_right: torch.Tensor | None = None,
+         stream=None) -> None:
+    """One Jacobi step of one tile (smi_stencil_step).  modes per side
+    (top, bottom, left, right): SIDE_COPY / SIDE_HALO / SIDE_SKIP."""
+    X, Y = inp.shape
+    m = (ctypes.c_int * 4)(*modes)
+    h = (ctypes.c_void_p * 4)(*[_ptr(t) for t in halos])
+    _lib.call("smi_stencil_step", inp.data_ptr(), out.data_ptr(), X, Y, m, h,
+              _ptr(send_left), _ptr(send_right), _lib.stream_handle(stream))
+
+
+def run(comm: Comm, tile: torch.Tensor, timesteps: int, PX: int, PY: int,
+        scratch: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """The whole stencil_smi run on this rank's tile (smi_stencil_run):
+    returns the tensor (tile or scratch) holding the result, like the
+    reference's copy-back of half timesteps%2 (stencil_smi.cpp:344)."""
+    if scratch is None:
+        scratch = torch.empty_like(tile)
+    X, Y = tile.shape
+    idx = ctypes.c_int()
+    _lib.call("smi_stencil_run", comm.handle, tile.data_ptr(), scratch.data_ptr(), X, Y, PX, PY,
+              timesteps, _lib.stream_handle(stream), ctypes.byref(idx))
+    return tile if idx.value == 0 else scratch
+
+
+def set_tuning(rows_per_wave: int = 0, rows_in_flight: int = 0, nontemporal: int = -1,
+               overlap: int = -1) -> None:
+    _lib.call("smi_stencil_set_tuning", rows_per_wave, rows_in_flight, nontemporal, overlap)
+
+
+def get_tuning() -> dict:
+    v = [ctypes.c_int() for _ in range(4)]
+    _lib.call("smi_stencil_get_tuning", *[ctypes.byref(x) for x in v])
+    return dict(rows_per_wave=v[0].value, rows_in_flight=v[1].value, nontemporal=v[2].value,
+                overlap=v[3].value)

@@ -1,0 +1,195 @@
+"""Stencil parity on the GPU: HIP sweep (through the C ABI) vs the CPU oracle.
+
+Contract: bit-exact fp32 against the device order 0.25*(((S+W)+E)+N) with
+global-edge cells copied (examples/kernels/stencil_smi.cl:117-165), for every
+tile shape, side mode, decomposition and tuning setting.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def run_steps(grid, T, **tune):
+    from smi_amd import stencil
+    if tune:
+        old = stencil.get_tuning()
+        stencil.set_tuning(**tune)
+    try:
+        a = torch.from_numpy(grid).cuda()
+        b = torch.empty_like(a)
+        for _ in range(T):
+            stencil.step(a, b)
+            a, b = b, a
+        torch.cuda.synchronize()
+        return a.cpu().numpy()
+    finally:
+        if tune:
+            stencil.set_tuning(old["rows_per_wave"], old["rows_in_flight"], old["nontemporal"],
+                               old["overlap"])
+
+
+SHAPES = [(1, 4), (2, 4), (3, 8), (5, 12), (7, 260), (64, 64), (129, 260), (256, 256), (300, 1028),
+          (1000, 516)]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("init", ["edges", "uniform"])
+def test_step_matches_oracle(gpu, oracle_mod, shape, init):
+    X, Y = shape
+    g = oracle_mod.init_edges(X, Y) if init == "edges" else oracle_mod.init_uniform(X, Y, seed=X * 31 + Y)
+    for T in (1, 3):
+        got = run_steps(g, T)
+        want = oracle_mod.stencil(g, T)
+        assert np.array_equal(bits(got), bits(want)), f"{shape} T={T}"
+
+
+def test_config1_grid_256_t32(gpu, oracle_mod):
+    """BASELINE config 1 problem (256x256, 32 steps) on one tile: bit-exact vs
+    the oracle and accepted by the reference host check (stencil_smi.cpp:391-405)."""
+    from smi_amd import stencil
+    g = stencil.init_grid(256, 256)
+    got = run_steps(g, 32)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 32)))
+    assert oracle_mod.reference_check(got, oracle_mod.stencil(g, 32, order="host"))
+
+
+@pytest.mark.parametrize("tune", [
+    dict(rows_per_wave=1, rows_in_flight=1), dict(rows_per_wave=7, rows_in_flight=2),
+    dict(rows_per_wave=64, rows_in_flight=8), dict(rows_per_wave=33, rows_in_flight=4, nontemporal=1),
+    dict(rows_per_wave=256, rows_in_flight=8, nontemporal=1)])
+def test_tuning_is_bit_neutral(gpu, oracle_mod, tune):
+    g = oracle_mod.init_uniform(517, 1540, seed=7)
+    assert np.array_equal(bits(run_steps(g, 2, **tune)), bits(oracle_mod.stencil(g, 2)))
+
+
+def _ext_reference(oracle_mod, tile, halos, modes):
+    """A HALO-mode step equals a full-grid step on the tile extended by its
+    halo ring (corners never read); COPY sides are global edges."""
+    X, Y = tile.shape
+    ext = np.zeros((X + 2, Y + 2), dtype=np.float32)
+    ext[1:-1, 1:-1] = tile
+    ext[0, 1:-1] = halos[0]
+    ext[-1, 1:-1] = halos[1]
+    ext[1:-1, 0] = halos[2]
+    ext[1:-1, -1] = halos[3]
+    ref = oracle_mod.stencil(ext, 1)[1:-1, 1:-1].copy()
+    # COPY sides keep their input cells
+    if modes[0] == 0:
+        ref[0, :] = tile[0, :]
+    if modes[1] == 0:
+        ref[-1, :] = tile[-1, :]
+    if modes[2] == 0:
+        ref[:, 0] = tile[:, 0]
+    if modes[3] == 0:
+        ref[:, -1] = tile[:, -1]
+    return ref
+
+
+@pytest.mark.parametrize("modes", [(1, 1, 1, 1), (0, 1, 0, 1), (1, 0, 1, 0), (0, 0, 1, 1), (1, 1, 0, 0)])
+@pytest.mark.parametrize("shape", [(1, 4), (6, 8), (70, 516), (257, 1024)])
+def test_halo_modes(gpu, oracle_mod, modes, shape):
+    from smi_amd import stencil
+    X, Y = shape
+    rng = np.random.default_rng(X + Y)
+    tile = rng.random((X, Y), dtype=np.float32)
+    halos = [rng.random(Y, dtype=np.float32), rng.random(Y, dtype=np.float32),
+             rng.random(X, dtype=np.float32), rng.random(X, dtype=np.float32)]
+    want = _ext_reference(oracle_mod, tile, halos, modes)
+    a = torch.from_numpy(tile).cuda()
+    out = torch.full_like(a, -7.0)
+    hd = [torch.from_numpy(h).cuda() if m == 1 else None for h, m in zip(halos, modes)]
+    sl = torch.zeros(X, device="cuda")
+    sr = torch.zeros(X, device="cuda")
+    stencil.step(a, out, modes, hd, sl, sr)
+    got = out.cpu().numpy()
+    assert np.array_equal(bits(got), bits(want))
+    assert np.array_equal(bits(sl.cpu().numpy()), bits(want[:, 0]))
+    assert np.array_equal(bits(sr.cpu().numpy()), bits(want[:, -1]))
+
+
+def test_skip_mode_leaves_cells(gpu, oracle_mod):
+    from smi_amd import stencil
+    X, Y = 40, 520
+    tile = oracle_mod.init_uniform(X, Y, seed=3)
+    halos = [torch.rand(Y, device="cuda"), torch.rand(Y, device="cuda"), torch.rand(X, device="cuda"),
+             torch.rand(X, device="cuda")]
+    a = torch.from_numpy(tile).cuda()
+    out = torch.full_like(a, -7.0)
+    stencil.step(a, out, (2, 2, 2, 2), halos)
+    got = out.cpu().numpy()
+    assert (got[0, :] == -7).all() and (got[-1, :] == -7).all()
+    assert (got[:, 0] == -7).all() and (got[:, -1] == -7).all()
+    ref = _ext_reference(oracle_mod, tile, [h.cpu().numpy() for h in halos], (1, 1, 1, 1))
+    assert np.array_equal(bits(got[1:-1, 1:-1]), bits(ref[1:-1, 1:-1]))
+
+
+def test_bad_arguments_raise(gpu):
+    from smi_amd import SMIError, stencil
+    a = torch.zeros((8, 6), device="cuda")  # y_local % 4 != 0
+    with pytest.raises(SMIError):
+        stencil.step(a, torch.empty_like(a))
+    b = torch.zeros((8, 8), device="cuda")
+    with pytest.raises(SMIError):
+        stencil.step(b, b)  # in == out
+    with pytest.raises(SMIError):
+        stencil.step(b, torch.empty_like(b), (1, 0, 0, 0))  # HALO side without halo
+
+
+def _decomposed_run(grid, T, PX, PY, overlap):
+    from smi_amd import LocalGroup, stencil
+    stencil.set_tuning(overlap=overlap)
+    tiles = stencil.split_memory(grid, PX, PY)
+
+    def rank_fn(comm):
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            t = torch.from_numpy(tiles[comm.rank]).cuda()
+            res = stencil.run(comm, t, T, PX, PY)
+            s.synchronize()
+            return res.cpu().numpy()
+
+    out = LocalGroup(PX * PY).run(rank_fn)
+    stencil.set_tuning(overlap=1)
+    return stencil.combine_memory(out, PX, PY)
+
+
+@pytest.mark.parametrize("overlap", [0, 1])
+@pytest.mark.parametrize("pxpy", [(1, 1), (2, 1), (1, 2), (2, 2), (2, 4), (4, 2)])
+def test_decomposed_matches_single(gpu, oracle_mod, pxpy, overlap):
+    PX, PY = pxpy
+    g = oracle_mod.init_uniform(64 * PX, 128 * PY, seed=PX * 10 + PY)
+    got = _decomposed_run(g, 9, PX, PY, overlap)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 9)))
+
+
+def test_config1_emulator_program(gpu, oracle_mod):
+    """BASELINE config 1 exactly: 4 ranks (PX=PY=2), 256x256 fp32, 32 steps,
+    reference init; bit-exact vs the rank-decomposed oracle and accepted by
+    the reference host check."""
+    from smi_amd import stencil
+    g = stencil.init_grid(256, 256)
+    got = _decomposed_run(g, 32, 2, 2, 1)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil_decomposed(g, 32, 2, 2)))
+    assert oracle_mod.reference_check(got, oracle_mod.stencil(g, 32, order="host"))
+
+
+def test_zero_timesteps_and_tiny_tiles(gpu, oracle_mod):
+    g = oracle_mod.init_uniform(8, 16, seed=1)
+    got = _decomposed_run(g, 0, 2, 2, 1)
+    assert np.array_equal(bits(got), bits(g))
+    g = oracle_mod.init_uniform(2, 8, seed=2)   # 1-row x 4-col tiles
+    got = _decomposed_run(g, 5, 2, 2, 1)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 5)))
+
+
+def test_full_size_8192_sweep(gpu, oracle_mod):
+    """BASELINE config 2 size (8192^2): two steps vs the threaded oracle."""
+    g = oracle_mod.init_uniform(8192, 8192, seed=42)
+    got = run_steps(g, 2)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 2)))
