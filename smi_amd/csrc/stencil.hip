@@ -246,9 +246,9 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *in, int row
 
 // ---------------------------------------------------------------- host --
 struct Tuning {
-    int ht = 64;        // rows per wave
-    int u = 4;          // rows in flight per batch
-    int nt = 0;         // non-temporal stores
+    int ht = 16;        // rows per wave
+    int u = 8;          // rows in flight per batch
+    int nt = 1;         // non-temporal stores
     int overlap = 1;    // overlap halo exchange with the interior sweep
 };
 static Tuning g_tune;
@@ -286,6 +286,7 @@ static int launch_sweep(const SweepArgs &a, hipStream_t s) {
     case 1: launch_sweep_u<1>(a, nstrips, nrb, ht, blocks, g_tune.nt, s); break;
     case 2: launch_sweep_u<2>(a, nstrips, nrb, ht, blocks, g_tune.nt, s); break;
     case 8: launch_sweep_u<8>(a, nstrips, nrb, ht, blocks, g_tune.nt, s); break;
+    case 16: launch_sweep_u<16>(a, nstrips, nrb, ht, blocks, g_tune.nt, s); break;
     default: launch_sweep_u<4>(a, nstrips, nrb, ht, blocks, g_tune.nt, s); break;
     }
     SMI_HIP_CHECK(hipGetLastError());
@@ -347,8 +348,8 @@ int smi_stencil_set_tuning(int rows_per_wave, int rows_in_flight, int nontempora
     if (rows_per_wave > 0) g_tune.ht = rows_per_wave;
     if (rows_in_flight > 0) {
         SMI_ARG_CHECK(rows_in_flight == 1 || rows_in_flight == 2 || rows_in_flight == 4 ||
-                          rows_in_flight == 8,
-                      "rows_in_flight must be 1, 2, 4 or 8");
+                          rows_in_flight == 8 || rows_in_flight == 16,
+                      "rows_in_flight must be 1, 2, 4, 8 or 16");
         g_tune.u = rows_in_flight;
     }
     if (nontemporal_stores >= 0) g_tune.nt = nontemporal_stores != 0;

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 outputs into profiles/.
+
+  pmc_summarize.py kt   <kernel_stats.csv> <out.json>
+  pmc_summarize.py pmc  <fetch_counter_collection.csv> <write_counter_collection.csv> <cells> <out.json>
+
+HBM bytes per launch follow MI355X_MICROARCH.md "HBM": FETCH_SIZE/WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide (16 B/lane)
+coalesced streaming read, so it is doubled; WRITE_SIZE is exact for 16-B
+streaming stores.
+"""
+import csv
+import json
+import sys
+
+KERNEL = "sweep_kernel"
+
+
+def rows(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def counter_per_dispatch(path, name):
+    vals = {}
+    for r in rows(path):
+        kn = r.get("Kernel_Name") or r.get("KernelName") or ""
+        if KERNEL not in kn:
+            continue
+        if r.get("Counter_Name") != name:
+            continue
+        did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+        vals[did] = vals.get(did, 0.0) + float(r["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    mode = sys.argv[1]
+    if mode == "kt":
+        out = []
+        for r in rows(sys.argv[2]):
+            out.append({k: r[k] for k in r})
+        json.dump(out, open(sys.argv[3], "w"), indent=1)
+        return
+    fetch = counter_per_dispatch(sys.argv[2], "FETCH_SIZE")
+    write = counter_per_dispatch(sys.argv[3], "WRITE_SIZE")
+    cells = int(sys.argv[4])
+    f = sorted(fetch)[len(fetch) // 2]
+    w = sorted(write)[len(write) // 2]
+    d = {
+        "kernel": KERNEL,
+        "cells": cells,
+        "dispatches": [len(fetch), len(write)],
+        "FETCH_SIZE_KiB_median": f,
+        "WRITE_SIZE_KiB_median": w,
+        "read_bytes_corrected": 2 * f * 1024,
+        "write_bytes": w * 1024,
+        "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
+        "algorithmic_bytes_per_launch": 8 * cells,
+        "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 counts half of wide coalesced reads)",
+    }
+    json.dump(d, open(sys.argv[5], "w"), indent=1)
+    print(json.dumps(d))
+
+
+if __name__ == "__main__":
+    main()

@@ -31,7 +31,7 @@ def main():
     torch.cuda.synchronize()
     copy_ms = e0.elapsed_time(e1) / steps
     print(json.dumps({"torch_copy_ms": copy_ms, "GBs": 8 * n * n / copy_ms / 1e6}), flush=True)
-    settings = list(itertools.product([16, 32, 64, 128, 256], [2, 4, 8], [0, 1]))
+    settings = list(itertools.product([8, 12, 16, 24, 32, 48], [4, 8, 16], [0, 1]))
     res = {s: [] for s in settings}
     for rnd in range(3):
         for (ht, u, nt) in settings:
