@@ -246,8 +246,8 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *in, int row
 
 // ---------------------------------------------------------------- host --
 struct Tuning {
-    int ht = 16;        // rows per wave
-    int u = 8;          // rows in flight per batch
+    int ht = 12;        // rows per wave
+    int u = 16;         // rows in flight per batch
     int nt = 1;         // non-temporal stores
     int overlap = 1;    // overlap halo exchange with the interior sweep
 };
@@ -447,15 +447,29 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     a.send_right = nb.right >= 0 ? s_right : nullptr;
     if (timesteps == 0) return SMI_SUCCESS;
 
-    hipEvent_t ev_edge, ev_comm;
+    // Schedule (two streams, no host synchronisation between steps):
+    //   comm stream : [wait int(t-1)] edge(t) -> rec E_edge(t) -> exchange(t)
+    //   main stream : [wait E_edge(t-1)] interior(t) -> rec E_int(t)
+    // edge(t) reads in(t) (interior cells from interior(t-1), halo-facing
+    // cells from edge(t-1)) and the halos received by exchange(t-1);
+    // interior(t) reads only in(t) and never a halo vector, so neither the
+    // edge kernel nor the xGMI exchange sits on the main stream's path.
+    hipEvent_t ev_edge, ev_int;
     SMI_TRY(comm_event(c, 0, &ev_edge));
-    SMI_TRY(comm_event(c, 1, &ev_comm));
+    SMI_TRY(comm_event(c, 1, &ev_int));
+    hipStream_t cs = c->comm_stream;
 
     // initial halos = the neighbours' initial edges (artificial step t=0)
-    hipLaunchKernelGGL(pack_cols_kernel, dim3((rows + 255) / 256), dim3(256), 0, s, buf0, rows, cols,
+    SMI_HIP_CHECK(hipEventRecord(ev_int, s));
+    SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
+    hipLaunchKernelGGL(pack_cols_kernel, dim3((rows + 255) / 256), dim3(256), 0, cs, buf0, rows, cols,
                        a.send_left, a.send_right);
     SMI_HIP_CHECK(hipGetLastError());
-    SMI_TRY(exchange(c, nb, buf0, rows, cols, h_top, h_bot, h_left, h_right, s_left, s_right, s));
+    SMI_TRY(exchange(c, nb, buf0, rows, cols, h_top, h_bot, h_left, h_right, s_left, s_right, cs));
+    if (!g_tune.overlap) {  // the full sweep reads the halos on the main stream
+        SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
+        SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
+    }
 
     SweepArgs inner = a;  // interior launch: halo-facing sides left to the edge kernel
     for (int k = 0; k < 4; ++k)
@@ -469,22 +483,31 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
         a.in = inner.in = in;
         a.out = inner.out = out;
         if (g_tune.overlap) {
-            SMI_TRY(launch_edge(a, side_mask, s));
-            SMI_HIP_CHECK(hipEventRecord(ev_edge, s));
+            // comm stream: halo-facing cells, then the exchange
+            SMI_TRY(launch_edge(a, side_mask, cs));
+            SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
+            if (!last)
+                SMI_TRY(exchange(c, nb, out, rows, cols, h_top, h_bot, h_left, h_right, s_left, s_right, cs));
+            // main stream: the interior, concurrently
             SMI_TRY(launch_sweep(inner, s));
-            if (!last) {
-                SMI_HIP_CHECK(hipStreamWaitEvent(c->comm_stream, ev_edge, 0));
-                SMI_TRY(exchange(c, nb, out, rows, cols, h_top, h_bot, h_left, h_right, s_left, s_right,
-                                 c->comm_stream));
-                SMI_HIP_CHECK(hipEventRecord(ev_comm, c->comm_stream));
-                SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_comm, 0));
-            }
+            SMI_HIP_CHECK(hipEventRecord(ev_int, s));
+            // next step: interior(t+1) needs edge(t); edge(t+1) needs interior(t)
+            SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
+            SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
         } else {
             SMI_TRY(launch_sweep(a, s));
-            if (!last)
-                SMI_TRY(exchange(c, nb, out, rows, cols, h_top, h_bot, h_left, h_right, s_left, s_right, s));
+            SMI_HIP_CHECK(hipEventRecord(ev_int, s));
+            if (!last) {
+                SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
+                SMI_TRY(exchange(c, nb, out, rows, cols, h_top, h_bot, h_left, h_right, s_left, s_right, cs));
+                SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
+                SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
+            }
         }
     }
+    // the caller's stream owns the result: join the comm stream
+    SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
+    SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
     return SMI_SUCCESS;
 }
 
