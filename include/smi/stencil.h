@@ -52,7 +52,8 @@ int smi_stencil_step(const float *in, float *out, int x_local, int y_local,
  * dedicated stream, overlapped with the interior sweep.  buf0 holds the
  * initial tile; buf1 is scratch of the same size.  On return *result_index
  * (0 or 1) names the buffer holding the final tile (like the reference's
- * half timesteps%2, stencil_smi.cpp:344).  Asynchronous w.r.t. the host
+ * half timesteps%2, stencil_smi.cpp:344; with two-step fusion the index is
+ * (pairs + remaining single steps) % 2).  Asynchronous w.r.t. the host
  * except for transport rendezvous. */
 int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local,
                     int y_local, int px, int py, int timesteps,
@@ -65,6 +66,15 @@ int smi_stencil_set_tuning(int rows_per_wave, int rows_in_flight,
                            int nontemporal_stores, int overlap);
 int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
                            int *nontemporal_stores, int *overlap);
+
+/* Temporal blocking: steps_per_pass = 2 fuses two Jacobi steps into one
+ * pass over HBM (same per-cell arithmetic, bit-identical result; multi-rank
+ * runs then exchange depth-2 halos -- two rows/columns per side neighbour
+ * and one corner cell per diagonal neighbour -- once per pair of steps).
+ * rows_per_wave / rows_in_flight tune the fused kernel (1, 2, 4 or 8).
+ * Tiles smaller than 4 x 8 always run single steps.  Pass <= 0 to keep. */
+int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_flight);
+int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in_flight);
 
 #ifdef __cplusplus
 }

@@ -17,62 +17,9 @@
 // and the interior sweep overlaps it.
 #include <algorithm>
 
-#include "smi_internal.h"
+#include "stencil_common.h"
 
 namespace smi {
-
-struct SweepArgs {
-    const float *in;
-    float *out;
-    int rows, cols;
-    int mode[4];            // SMI_SIDE_* per side: top, bottom, left, right
-    const float *halo[4];   // halo vectors for SMI_SIDE_HALO sides
-    float *send_left;       // packed new first column (nullable)
-    float *send_right;      // packed new last column (nullable)
-};
-
-// 0.25 * (((S + W) + E) + N), fp32, round-to-nearest, never contracted
-// (stencil_smi.cl:153-156; 0.25*x is exact, so the double literal there
-// gives the same bits as this fp32 multiply).
-__device__ __forceinline__ float jacobi(float s, float w, float e, float n) {
-    float sum = __fadd_rn(s, w);
-    sum = __fadd_rn(sum, e);
-    sum = __fadd_rn(sum, n);
-    return __fmul_rn(0.25f, sum);
-}
-
-// lane i <- lane i-1 (DPP wave_shr:1); lane 0 gets 0
-__device__ __forceinline__ float wave_shr1(float v) {
-    return __builtin_bit_cast(
-        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
-}
-// lane i <- lane i+1 (DPP wave_shl:1); lane 63 gets 0
-__device__ __forceinline__ float wave_shl1(float v) {
-    return __builtin_bit_cast(
-        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
-}
-
-// Blocks b, b+8, b+16 ... share an XCD (round-robin dispatch); give each XCD
-// a contiguous range of logical blocks so that vertically and horizontally
-// adjacent strips -- whose edge rows/cells each reads -- share one L2.
-// Bijective for any nb (cdna_hip_programming.md, "XCD swizzle").
-__device__ __forceinline__ int xcd_remap(int b, int nb) {
-    const int q = nb >> 3, r = nb & 7, x = b & 7;
-    const int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-    return base + (b >> 3);
-}
-
-template <bool NT>
-__device__ __forceinline__ void store4(float *p, float4 v) {
-    if constexpr (NT) {
-        __builtin_nontemporal_store(v.x, p + 0);
-        __builtin_nontemporal_store(v.y, p + 1);
-        __builtin_nontemporal_store(v.z, p + 2);
-        __builtin_nontemporal_store(v.w, p + 3);
-    } else {
-        *reinterpret_cast<float4 *>(p) = v;
-    }
-}
 
 // One wave = one strip of 256 columns x `ht` rows; 4 waves per block take 4
 // consecutive (row-block, strip) tasks, strip fastest.  U rows are fetched
@@ -245,17 +192,9 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *in, int row
 }
 
 // ---------------------------------------------------------------- host --
-struct Tuning {
-    int ht = 12;        // rows per wave
-    int u = 16;         // rows in flight per batch
-    int nt = 1;         // non-temporal stores
-    int overlap = 1;    // overlap halo exchange with the interior sweep
-};
-static Tuning g_tune;
+Tuning g_tune;
 
-static bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
-
-static int check_tile(const float *in, const float *out, int rows, int cols) {
+int check_tile(const float *in, const float *out, int rows, int cols) {
     SMI_ARG_CHECK(in && out, "NULL tile buffer");
     SMI_ARG_CHECK(in != out, "in and out must differ");
     SMI_ARG_CHECK(rows >= 1 && cols >= 4 && cols % 4 == 0, "tile must be >=1 x >=4 with y_local % 4 == 0");
@@ -274,7 +213,7 @@ static void launch_sweep_u(const SweepArgs &a, int nstrips, int nrb, int ht, int
                            nstrips, nrb, ht);
 }
 
-static int launch_sweep(const SweepArgs &a, hipStream_t s) {
+int launch_sweep(const SweepArgs &a, hipStream_t s) {
     const int ht = std::max(1, g_tune.ht);
     const int nstrips = (a.cols + 255) / 256;
     const int nrb = (a.rows + ht - 1) / ht;
@@ -294,7 +233,7 @@ static int launch_sweep(const SweepArgs &a, hipStream_t s) {
     return SMI_SUCCESS;
 }
 
-static int launch_edge(const SweepArgs &a, int side_mask, hipStream_t s) {
+int launch_edge(const SweepArgs &a, int side_mask, hipStream_t s) {
     const long cells = 2L * a.cols + 2L * a.rows;
     const int blocks = (int)((cells + 255) / 256);
     int tok = -1;
@@ -305,37 +244,10 @@ static int launch_edge(const SweepArgs &a, int side_mask, hipStream_t s) {
     return SMI_SUCCESS;
 }
 
-// Halo exchange of one step (Convert{Send,Receive}* of stencil_smi.cl:
-// 236-386 as one transport group): my new first/last row go to the rank
-// above/below, my packed first/last column to the left/right rank; the four
-// halo vectors are received from the same neighbours.
-struct Neighbours {
-    int top = -1, bottom = -1, left = -1, right = -1;
-};
-
-static int exchange(Comm *c, const Neighbours &nb, const float *tile, int rows, int cols,
-                    float *h_top, float *h_bot, float *h_left, float *h_right, const float *s_left,
-                    const float *s_right, hipStream_t s) {
-    Transport *tp = c->transport.get();
-    const size_t rb = (size_t)cols * sizeof(float), cb = (size_t)rows * sizeof(float);
-    SMI_TRY(tp->begin(s));
-    if (nb.top >= 0) {
-        SMI_TRY(tp->send(tile, rb, nb.top));
-        SMI_TRY(tp->recv(h_top, rb, nb.top));
-    }
-    if (nb.bottom >= 0) {
-        SMI_TRY(tp->send(tile + (size_t)(rows - 1) * cols, rb, nb.bottom));
-        SMI_TRY(tp->recv(h_bot, rb, nb.bottom));
-    }
-    if (nb.left >= 0) {
-        SMI_TRY(tp->send(s_left, cb, nb.left));
-        SMI_TRY(tp->recv(h_left, cb, nb.left));
-    }
-    if (nb.right >= 0) {
-        SMI_TRY(tp->send(s_right, cb, nb.right));
-        SMI_TRY(tp->recv(h_right, cb, nb.right));
-    }
-    return tp->end();
+int launch_pack_cols(const float *in, int rows, int cols, float *left, float *right, hipStream_t s) {
+    hipLaunchKernelGGL(pack_cols_kernel, dim3((rows + 255) / 256), dim3(256), 0, s, in, rows, cols, left, right);
+    SMI_HIP_CHECK(hipGetLastError());
+    return SMI_SUCCESS;
 }
 
 }  // namespace smi
@@ -384,131 +296,6 @@ int smi_stencil_step(const float *in, float *out, int x_local, int y_local, cons
     a.send_left = send_left;
     a.send_right = send_right;
     return launch_sweep(a, (hipStream_t)stream);
-}
-
-int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_local, int px, int py,
-                    int timesteps, SMI_Stream stream_, int *result_index) {
-    Comm *c = lookup_comm(comm);
-    if (!c) {
-        set_error("unknown communicator");
-        return SMI_ERR_BAD_COMM;
-    }
-    SMI_TRY(check_tile(buf0, buf1, x_local, y_local));
-    SMI_ARG_CHECK(px >= 1 && py >= 1 && px * py == c->size, "px*py must equal the communicator size");
-    SMI_ARG_CHECK(timesteps >= 0, "timesteps < 0");
-    SMI_ARG_CHECK(result_index, "NULL result_index");
-    hipStream_t s = (hipStream_t)stream_;
-    const int rows = x_local, cols = y_local;
-    // rank -> (i_px, i_py) and neighbours, examples/host/stencil_smi.cpp:133-134
-    // and stencil_smi.cl:242,257,269,293,320,334,345,368
-    const int ipx = c->rank / py, ipy = c->rank % py;
-    Neighbours nb;
-    if (ipx > 0) nb.top = (ipx - 1) * py + ipy;
-    if (ipx < px - 1) nb.bottom = (ipx + 1) * py + ipy;
-    if (ipy > 0) nb.left = ipx * py + ipy - 1;
-    if (ipy < py - 1) nb.right = ipx * py + ipy + 1;
-    const int side_nb[4] = {nb.top, nb.bottom, nb.left, nb.right};
-
-    SweepArgs a{};
-    a.rows = rows;
-    a.cols = cols;
-    int side_mask = 0;
-    for (int k = 0; k < 4; ++k) {
-        a.mode[k] = side_nb[k] >= 0 ? SMI_SIDE_HALO : SMI_SIDE_COPY;
-        if (side_nb[k] >= 0) side_mask |= 1 << k;
-    }
-    *result_index = timesteps & 1;
-
-    if (side_mask == 0) {  // single tile: no exchange at all
-        for (int t = 0; t < timesteps; ++t) {
-            a.in = (t & 1) ? buf1 : buf0;
-            a.out = (t & 1) ? buf0 : buf1;
-            SMI_TRY(launch_sweep(a, s));
-        }
-        return SMI_SUCCESS;
-    }
-
-    // halo staging: recv top, bottom (cols each), left, right (rows each),
-    // send left, send right (rows each)
-    const size_t need = 2 * (size_t)cols + 4 * (size_t)rows;
-    if (c->halo_elems < need) {
-        if (c->halo) SMI_HIP_CHECK(hipFree(c->halo));
-        c->halo = nullptr;
-        SMI_HIP_CHECK(hipMalloc(&c->halo, need * sizeof(float)));
-        c->halo_elems = need;
-    }
-    float *h_top = c->halo, *h_bot = h_top + cols, *h_left = h_bot + cols, *h_right = h_left + rows;
-    float *s_left = h_right + rows, *s_right = s_left + rows;
-    a.halo[0] = h_top;
-    a.halo[1] = h_bot;
-    a.halo[2] = h_left;
-    a.halo[3] = h_right;
-    a.send_left = nb.left >= 0 ? s_left : nullptr;
-    a.send_right = nb.right >= 0 ? s_right : nullptr;
-    if (timesteps == 0) return SMI_SUCCESS;
-
-    // Schedule (two streams, no host synchronisation between steps):
-    //   comm stream : [wait int(t-1)] edge(t) -> rec E_edge(t) -> exchange(t)
-    //   main stream : [wait E_edge(t-1)] interior(t) -> rec E_int(t)
-    // edge(t) reads in(t) (interior cells from interior(t-1), halo-facing
-    // cells from edge(t-1)) and the halos received by exchange(t-1);
-    // interior(t) reads only in(t) and never a halo vector, so neither the
-    // edge kernel nor the xGMI exchange sits on the main stream's path.
-    hipEvent_t ev_edge, ev_int;
-    SMI_TRY(comm_event(c, 0, &ev_edge));
-    SMI_TRY(comm_event(c, 1, &ev_int));
-    hipStream_t cs = c->comm_stream;
-
-    // initial halos = the neighbours' initial edges (artificial step t=0)
-    SMI_HIP_CHECK(hipEventRecord(ev_int, s));
-    SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
-    hipLaunchKernelGGL(pack_cols_kernel, dim3((rows + 255) / 256), dim3(256), 0, cs, buf0, rows, cols,
-                       a.send_left, a.send_right);
-    SMI_HIP_CHECK(hipGetLastError());
-    SMI_TRY(exchange(c, nb, buf0, rows, cols, h_top, h_bot, h_left, h_right, s_left, s_right, cs));
-    if (!g_tune.overlap) {  // the full sweep reads the halos on the main stream
-        SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-        SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-    }
-
-    SweepArgs inner = a;  // interior launch: halo-facing sides left to the edge kernel
-    for (int k = 0; k < 4; ++k)
-        if (inner.mode[k] == SMI_SIDE_HALO) inner.mode[k] = SMI_SIDE_SKIP;
-    inner.send_left = inner.send_right = nullptr;
-
-    for (int t = 0; t < timesteps; ++t) {
-        const float *in = (t & 1) ? buf1 : buf0;
-        float *out = (t & 1) ? buf0 : buf1;
-        const bool last = t == timesteps - 1;
-        a.in = inner.in = in;
-        a.out = inner.out = out;
-        if (g_tune.overlap) {
-            // comm stream: halo-facing cells, then the exchange
-            SMI_TRY(launch_edge(a, side_mask, cs));
-            SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-            if (!last)
-                SMI_TRY(exchange(c, nb, out, rows, cols, h_top, h_bot, h_left, h_right, s_left, s_right, cs));
-            // main stream: the interior, concurrently
-            SMI_TRY(launch_sweep(inner, s));
-            SMI_HIP_CHECK(hipEventRecord(ev_int, s));
-            // next step: interior(t+1) needs edge(t); edge(t+1) needs interior(t)
-            SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-            SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
-        } else {
-            SMI_TRY(launch_sweep(a, s));
-            SMI_HIP_CHECK(hipEventRecord(ev_int, s));
-            if (!last) {
-                SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
-                SMI_TRY(exchange(c, nb, out, rows, cols, h_top, h_bot, h_left, h_right, s_left, s_right, cs));
-                SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-                SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-            }
-        }
-    }
-    // the caller's stream owns the result: join the comm stream
-    SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-    SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-    return SMI_SUCCESS;
 }
 
 }  // extern "C"

@@ -1,0 +1,102 @@
+// stencil_common.h -- shared pieces of the stencil kernels and driver.
+#pragma once
+
+#include <algorithm>
+
+#include "smi_internal.h"
+
+namespace smi {
+
+struct SweepArgs {
+    const float *in;
+    float *out;
+    int rows, cols;
+    int mode[4];            // SMI_SIDE_* per side: top, bottom, left, right
+    const float *halo[4];   // halo vectors for SMI_SIDE_HALO sides
+    float *send_left;       // packed new first column (nullable)
+    float *send_right;      // packed new last column (nullable)
+};
+
+// 0.25 * (((S + W) + E) + N), fp32, round-to-nearest, never contracted
+// (stencil_smi.cl:153-156; 0.25*x is exact, so the double literal there
+// gives the same bits as this fp32 multiply).
+__device__ __forceinline__ float jacobi(float s, float w, float e, float n) {
+    float sum = __fadd_rn(s, w);
+    sum = __fadd_rn(sum, e);
+    sum = __fadd_rn(sum, n);
+    return __fmul_rn(0.25f, sum);
+}
+
+// lane i <- lane i-1 (DPP wave_shr:1); lane 0 gets 0
+__device__ __forceinline__ float wave_shr1(float v) {
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+// lane i <- lane i+1 (DPP wave_shl:1); lane 63 gets 0
+__device__ __forceinline__ float wave_shl1(float v) {
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+}
+
+// Blocks b, b+8, b+16 ... share an XCD (round-robin dispatch); give each XCD
+// a contiguous range of logical blocks so that vertically and horizontally
+// adjacent strips -- whose edge rows/cells each reads -- share one L2.
+// Bijective for any nb (cdna_hip_programming.md, "XCD swizzle").
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+    const int q = nb >> 3, r = nb & 7, x = b & 7;
+    const int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    return base + (b >> 3);
+}
+
+template <bool NT>
+__device__ __forceinline__ void store4(float *p, float4 v) {
+    if constexpr (NT) {
+        __builtin_nontemporal_store(v.x, p + 0);
+        __builtin_nontemporal_store(v.y, p + 1);
+        __builtin_nontemporal_store(v.z, p + 2);
+        __builtin_nontemporal_store(v.w, p + 3);
+    } else {
+        *reinterpret_cast<float4 *>(p) = v;
+    }
+}
+
+struct Tuning {
+    int ht = 12;        // rows per wave (single-step sweep)
+    int u = 16;         // rows in flight per batch
+    int nt = 1;         // non-temporal stores
+    int overlap = 1;    // overlap halo exchange with the interior sweep
+    int fuse = 1;       // Jacobi steps per pass over HBM (1 or 2)
+    int ht2 = 32;       // rows per wave (two-step sweep)
+    int u2 = 8;         // rows in flight per batch (two-step sweep)
+};
+extern Tuning g_tune;
+
+inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+int check_tile(const float *in, const float *out, int rows, int cols);
+
+// single step (stencil.hip)
+int launch_sweep(const SweepArgs &a, hipStream_t s);
+int launch_edge(const SweepArgs &a, int side_mask, hipStream_t s);
+int launch_pack_cols(const float *in, int rows, int cols, float *left, float *right, hipStream_t s);
+
+// two steps per pass (stencil2.hip).  skip[k] = 1: the 2-wide ring on side k
+// has a neighbour and is computed by the ring kernel; 0: global edge (copy).
+struct Sweep2Args {
+    const float *in;
+    float *out;
+    int rows, cols;
+    int skip[4];
+};
+// depth-2 halos: top2 = rows -2,-1 (2 x cols); bot2 = rows X, X+1; left2 =
+// cols -2,-1 ([2][rows]); right2 = cols Y, Y+1; corner = (-1,-1), (-1,Y),
+// (X,-1), (X,Y).  send2 = packed cols 0,1 | cols Y-2,Y-1 ([2][rows] each) and
+// the 4 corner cells (0,0), (0,Y-1), (X-1,0), (X-1,Y-1).
+struct Halo2 {
+    const float *top2, *bot2, *left2, *right2, *corner;
+    float *send_left2, *send_right2, *send_corner;
+};
+int launch_sweep2(const Sweep2Args &a, hipStream_t s);
+int launch_ring2(const Sweep2Args &a, const Halo2 &h, hipStream_t s);
+int launch_pack2(const float *in, int rows, int cols, const Halo2 &h, hipStream_t s);
+
+}  // namespace smi

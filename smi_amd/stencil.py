@@ -95,3 +95,14 @@ def get_tuning() -> dict:
     _lib.call("smi_stencil_get_tuning", *[ctypes.byref(x) for x in v])
     return dict(rows_per_wave=v[0].value, rows_in_flight=v[1].value, nontemporal=v[2].value,
                 overlap=v[3].value)
+
+
+def set_fusion(steps_per_pass: int = 0, rows_per_wave: int = 0, rows_in_flight: int = 0) -> None:
+    """1 = one Jacobi step per pass over HBM, 2 = two fused steps (same bits)."""
+    _lib.call("smi_stencil_set_fusion", steps_per_pass, rows_per_wave, rows_in_flight)
+
+
+def get_fusion() -> dict:
+    v = [ctypes.c_int() for _ in range(3)]
+    _lib.call("smi_stencil_get_fusion", *[ctypes.byref(x) for x in v])
+    return dict(steps_per_pass=v[0].value, rows_per_wave=v[1].value, rows_in_flight=v[2].value)

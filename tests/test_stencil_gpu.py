@@ -193,3 +193,56 @@ def test_full_size_8192_sweep(gpu, oracle_mod):
     g = oracle_mod.init_uniform(8192, 8192, seed=42)
     got = run_steps(g, 2)
     assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 2)))
+
+
+# ------------------------------------------------ two steps per pass (fused) --
+def _run_fused(grid, T, PX=1, PY=1, overlap=1, ht2=0, u2=0):
+    from smi_amd import stencil
+    old = stencil.get_fusion()
+    stencil.set_fusion(2, ht2, u2)
+    try:
+        return _decomposed_run(grid, T, PX, PY, overlap)
+    finally:
+        stencil.set_fusion(old["steps_per_pass"], old["rows_per_wave"], old["rows_in_flight"])
+
+
+@pytest.mark.parametrize("shape", [(4, 8), (5, 8), (7, 260), (64, 64), (129, 260), (300, 1028), (1000, 516)])
+def test_fused_single_tile(gpu, oracle_mod, shape):
+    X, Y = shape
+    g = oracle_mod.init_uniform(X, Y, seed=X + 3 * Y)
+    for T in (1, 2, 3, 6):
+        got = _run_fused(g, T)
+        assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (shape, T)
+
+
+@pytest.mark.parametrize("ht2,u2", [(1, 1), (3, 2), (16, 4), (64, 8), (7, 8)])
+def test_fused_tuning_is_bit_neutral(gpu, oracle_mod, ht2, u2):
+    g = oracle_mod.init_uniform(517, 1540, seed=9)
+    got = _run_fused(g, 4, ht2=ht2, u2=u2)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 4)))
+
+
+@pytest.mark.parametrize("overlap", [0, 1])
+@pytest.mark.parametrize("pxpy", [(2, 1), (1, 2), (2, 2), (2, 4), (4, 2), (3, 3)])
+def test_fused_decomposed(gpu, oracle_mod, pxpy, overlap):
+    PX, PY = pxpy
+    g = oracle_mod.init_uniform(64 * PX, 128 * PY, seed=PX * 7 + PY)
+    for T in (5, 8):
+        got = _run_fused(g, T, PX, PY, overlap)
+        assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (pxpy, T)
+
+
+def test_fused_tiny_and_fallback_tiles(gpu, oracle_mod):
+    g = oracle_mod.init_uniform(8, 16, seed=21)     # 4x8 tiles at 2x2: smallest fused tile
+    assert np.array_equal(bits(_run_fused(g, 7, 2, 2)), bits(oracle_mod.stencil(g, 7)))
+    g = oracle_mod.init_uniform(6, 8, seed=22)      # 3x4 tiles: single-step fallback
+    assert np.array_equal(bits(_run_fused(g, 7, 2, 2)), bits(oracle_mod.stencil(g, 7)))
+    g = stencil_init = oracle_mod.init_edges(256, 256)   # config 1 through the fused path
+    got = _run_fused(g, 32, 2, 2)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil_decomposed(stencil_init, 32, 2, 2)))
+
+
+def test_fused_full_size_8192(gpu, oracle_mod):
+    g = oracle_mod.init_uniform(8192, 8192, seed=43)
+    got = _run_fused(g, 4)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 4)))
