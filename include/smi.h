@@ -16,9 +16,14 @@
 #include "smi/data_types.h"
 #include "smi/operation_type.h"
 #include "smi/communicator.h"
+#include "smi/channel_descriptor.h"
+#include "smi/push.h"
+#include "smi/pop.h"
 #include "smi/stencil.h"
 #include "smi/reduce.h"
 #include "smi/bcast.h"
+#include "smi/scatter.h"
+#include "smi/gather.h"
 #include "smi/gesummv.h"
 #include "smi/profiling.h"
 

@@ -1,0 +1,33 @@
+/*
+ * push.h -- send side of a point-to-point transient channel (host-callable).
+ *
+ * Same names and argument meaning as the reference include/smi/push.h:19-48
+ * (implementation codegen/templates/push.cl:3-70): elements are packed into
+ * packets (here 2032-byte payloads instead of 28-byte ones) and a packet is
+ * sent when it is full, when the message is complete, or on an immediate
+ * flush.  Sends are buffered (32 packets per communicator in flight), the
+ * counterpart of the reference's credit window, so a rank may push before its
+ * peer pops.  `data` points to ONE element in host memory.
+ */
+#ifndef SMI_PUSH_H
+#define SMI_PUSH_H
+
+#include "channel_descriptor.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+SMI_Channel SMI_Open_send_channel(int count, SMI_Datatype data_type, int destination, int port,
+                                  SMI_Comm comm);
+/* asynch_degree (elements) is accepted for source compatibility; buffering is
+ * fixed by the runtime's packet ring. */
+SMI_Channel SMI_Open_send_channel_ad(int count, SMI_Datatype data_type, int destination, int port,
+                                     SMI_Comm comm, int asynch_degree);
+void SMI_Push_flush(SMI_Channel *chan, void *data, int immediate);
+void SMI_Push(SMI_Channel *chan, void *data);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMI_PUSH_H */

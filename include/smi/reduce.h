@@ -19,6 +19,7 @@
 #include <stddef.h>
 #include "communicator.h"
 #include "data_types.h"
+#include "channel_descriptor.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -38,6 +39,18 @@ typedef enum {
 int smi_reduce(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count,
                SMI_Datatype type, SMI_Op op, int root, int port,
                SMI_Stream stream);
+
+/* Element API, same names and argument meaning as the reference
+ * (include/smi/reduce.h:55-76): every rank calls SMI_Reduce `count` times;
+ * the root receives each element's reduction in data_rcv on return.  The
+ * root folds the n contributions of the element with the same HIP fold
+ * kernel as smi_reduce (one launch per element: a compatibility path, use
+ * smi_reduce for throughput). */
+SMI_RChannel SMI_Open_reduce_channel(int count, SMI_Datatype data_type, SMI_Op op, int port, int root,
+                                     SMI_Comm comm);
+SMI_RChannel SMI_Open_reduce_channel_ad(int count, SMI_Datatype data_type, SMI_Op op, int port, int root,
+                                        SMI_Comm comm, int asynch_degree);
+void SMI_Reduce(SMI_RChannel *chan, void *data_snd, void *data_rcv);
 
 /* The local fold kernel: contribs holds `nranks` rows of `count` elements
  * (row r = rank r's contribution, row pitch `ld` elements); out[i] = fold of

@@ -12,6 +12,6 @@ from ._lib import (  # noqa: F401
     SIDE_COPY, SIDE_HALO, SIDE_SKIP, SMIError, load,
 )
 from .comm import Comm, LocalGroup  # noqa: F401
-from . import stencil, collectives, gesummv, profiling  # noqa: F401
+from . import stencil, collectives, gesummv, profiling, channels  # noqa: F401
 
-__all__ = ["Comm", "LocalGroup", "stencil", "collectives", "gesummv", "profiling", "SMIError", "load"]
+__all__ = ["Comm", "LocalGroup", "stencil", "collectives", "gesummv", "profiling", "channels", "SMIError", "load"]

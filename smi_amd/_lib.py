@@ -65,6 +65,8 @@ SIGNATURES = {
     "smi_reduce_fold": (I, [P, P, I, SZ, SZ, I, I, P]),
     "smi_bcast": (I, [SMI_Comm, P, SZ, I, I, I, P]),
     "smi_type_size": (SZ, [I]),
+    "smi_scatter": (I, [SMI_Comm, P, P, SZ, I, I, I, P]),
+    "smi_gather": (I, [SMI_Comm, P, P, SZ, I, I, I, P]),
     "smi_gemv_rows": (I, [P, P, P, P, I, I, I, F, F, P]),
     "smi_gesummv": (I, [SMI_Comm, P, P, P, P, I, I, F, F, I, P]),
     "smi_prof_enable": (I, [I]),
@@ -88,7 +90,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
             raise SMIError(f"{path} missing: run smi_amd.build.build()")
         _build.build()
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
-    for name, (res, args) in SIGNATURES.items():
+    for name, (res, args) in list(SIGNATURES.items()):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

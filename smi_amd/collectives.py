@@ -57,3 +57,18 @@ def reduce_fold(contribs: torch.Tensor, op="add", out: torch.Tensor | None = Non
     _lib.call("smi_reduce_fold", contribs.data_ptr(), out.data_ptr(), n, count, contribs.stride(0),
               _smi_type(contribs), _op(op), _lib.stream_handle(stream))
     return out
+
+
+def scatter(comm: Comm, send: torch.Tensor | None, recv: torch.Tensor, root: int = 0, port: int = 0,
+            stream=None) -> None:
+    """Root's `send` (size*count elements) split over the ranks' `recv`."""
+    _lib.call("smi_scatter", comm.handle, None if send is None else send.data_ptr(), recv.data_ptr(),
+              recv.numel(), _smi_type(recv), root, port, _lib.stream_handle(stream))
+
+
+def gather(comm: Comm, send: torch.Tensor, recv: torch.Tensor | None, root: int = 0, port: int = 0,
+           stream=None) -> None:
+    """Every rank's `send` (count elements) concatenated in rank order in the
+    root's `recv`."""
+    _lib.call("smi_gather", comm.handle, send.data_ptr(), None if recv is None else recv.data_ptr(),
+              send.numel(), _smi_type(send), root, port, _lib.stream_handle(stream))

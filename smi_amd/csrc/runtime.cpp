@@ -198,6 +198,7 @@ int smi_finalize(SMI_Comm comm) {
     SMI_HIP_CHECK(hipSetDevice(c->device));
     if (c->comm_stream) SMI_HIP_CHECK(hipStreamSynchronize(c->comm_stream));
     SMI_HIP_CHECK(hipDeviceSynchronize());
+    c->chan_engine.reset();
     c->transport.reset();
     for (auto e : c->events) SMI_HIP_CHECK(hipEventDestroy(e));
     if (c->work) SMI_HIP_CHECK(hipFree(c->work));

@@ -47,6 +47,16 @@ void set_error(const std::string &msg);
 // of a group are ordered after the work already queued on `stream`, and work
 // queued on `stream` after end() observes every receive of the group and may
 // overwrite every send buffer of the group.
+// A detached send (used by the element-granular channels) returns at once;
+// the ticket completes when the bytes have left the send buffer, so the
+// sender can keep pushing while the receiver has not popped yet -- the
+// buffering the reference gets from its credit window (push.cl:21-31).
+struct SendTicket {
+    std::shared_ptr<void> impl;
+    hipEvent_t ev = nullptr;
+    bool live = false;
+};
+
 class Transport {
   public:
     virtual ~Transport() = default;
@@ -54,6 +64,11 @@ class Transport {
     virtual int send(const void *buf, size_t bytes, int peer) = 0;
     virtual int recv(void *buf, size_t bytes, int peer) = 0;
     virtual int end() = 0;
+    virtual int send_detached(const void *buf, size_t bytes, int peer, hipStream_t stream, SendTicket *t) = 0;
+    virtual int ticket_wait(SendTicket *t) = 0;
+    // One receive, enqueued on `stream` (the caller synchronises).  Like
+    // send_detached, safe to call from several host threads at once.
+    virtual int recv_now(void *buf, size_t bytes, int peer, hipStream_t stream) = 0;
 };
 
 std::unique_ptr<Transport> make_rccl_transport(int rank, int size,
@@ -77,6 +92,7 @@ struct Comm {
     float *halo = nullptr;
     size_t halo_elems = 0;
     std::vector<hipEvent_t> events;  // reusable sync events
+    std::shared_ptr<void> chan_engine;  // element-granular channels (channels.cpp)
 };
 
 Comm *lookup_comm(SMI_Comm c);

@@ -43,6 +43,32 @@ class RcclTransport final : public Transport {
     }
     int end() override { return check(ncclGroupEnd(), "ncclGroupEnd"); }
 
+    // Small sends complete into the peer's connection FIFO without a posted
+    // receive, so a detached send only needs an event to tell when the
+    // staging buffer may be reused.
+    int send_detached(const void *buf, size_t bytes, int peer, hipStream_t stream, SendTicket *t) override {
+        std::lock_guard<std::mutex> lk(mu_);  // RCCL communicators are not thread-safe
+        SMI_TRY(check(ncclGroupStart(), "ncclGroupStart"));
+        SMI_TRY(check(ncclSend(buf, bytes, ncclUint8, peer, comm_, stream), "ncclSend"));
+        SMI_TRY(check(ncclGroupEnd(), "ncclGroupEnd"));
+        if (!t->ev) SMI_HIP_CHECK(hipEventCreateWithFlags(&t->ev, hipEventDisableTiming));
+        SMI_HIP_CHECK(hipEventRecord(t->ev, stream));
+        t->live = true;
+        return SMI_SUCCESS;
+    }
+    int ticket_wait(SendTicket *t) override {
+        if (!t->live) return SMI_SUCCESS;
+        SMI_HIP_CHECK(hipEventSynchronize(t->ev));
+        t->live = false;
+        return SMI_SUCCESS;
+    }
+    int recv_now(void *buf, size_t bytes, int peer, hipStream_t stream) override {
+        std::lock_guard<std::mutex> lk(mu_);
+        SMI_TRY(check(ncclGroupStart(), "ncclGroupStart"));
+        SMI_TRY(check(ncclRecv(buf, bytes, ncclUint8, peer, comm_, stream), "ncclRecv"));
+        return check(ncclGroupEnd(), "ncclGroupEnd");
+    }
+
     static int check(ncclResult_t r, const char *what) {
         if (r == ncclSuccess) return SMI_SUCCESS;
         set_error(std::string(what) + ": " + ncclGetErrorString(r));
@@ -52,6 +78,7 @@ class RcclTransport final : public Transport {
   private:
     ncclComm_t comm_ = nullptr;
     hipStream_t stream_ = nullptr;
+    std::mutex mu_;
 };
 
 std::unique_ptr<Transport> make_rccl_transport(int rank, int size,
@@ -160,35 +187,8 @@ class LocalTransport final : public Transport {
 
         int rc = SMI_SUCCESS;
         for (auto &r : recvs_) {
-            std::shared_ptr<Post> p;
-            {
-                std::unique_lock<std::mutex> lk(g_->mu);
-                auto &q = g_->mailbox[{r.peer, rank_}];
-                g_->cv.wait(lk, [&] { return !q.empty(); });
-                p = q.front();
-                q.pop_front();
-            }
-            int st = SMI_SUCCESS;
-            if (p->bytes != r.bytes) {
-                set_error("local transport: send/recv size mismatch");
-                st = SMI_ERR_COMM;
-            } else {
-                if (hipStreamWaitEvent(stream_, p->ready, 0) != hipSuccess ||
-                    (r.bytes && hipMemcpyAsync(r.buf, p->buf, r.bytes, hipMemcpyDeviceToDevice,
-                                               stream_) != hipSuccess))
-                    st = SMI_ERR_HIP;
-            }
-            if (hipEventRecord(p->done, stream_) != hipSuccess && st == SMI_SUCCESS) st = SMI_ERR_HIP;
-            {
-                std::lock_guard<std::mutex> lk(g_->mu);
-                p->status = st;
-                p->copied = true;
-            }
-            g_->cv.notify_all();
-            if (st != SMI_SUCCESS && rc == SMI_SUCCESS) {
-                if (st == SMI_ERR_HIP) set_error("local transport: HIP copy failed");
-                rc = st;
-            }
+            const int st = take(r.buf, r.bytes, r.peer, stream_);
+            if (st != SMI_SUCCESS && rc == SMI_SUCCESS) rc = st;
         }
         for (auto &p : mine) {
             {
@@ -209,7 +209,83 @@ class LocalTransport final : public Transport {
         return rc;
     }
 
+    // Post the send and return; the peer's receive performs the copy later.
+    int send_detached(const void *buf, size_t bytes, int peer, hipStream_t stream, SendTicket *t) override {
+        if (peer < 0 || peer >= g_->size) {
+            set_error("send: peer out of range");
+            return SMI_ERR_INVALID_ARG;
+        }
+        auto p = std::make_shared<Post>();
+        p->buf = buf;
+        p->bytes = bytes;
+        SMI_HIP_CHECK(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
+        SMI_HIP_CHECK(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
+        SMI_HIP_CHECK(hipEventRecord(p->ready, stream));
+        {
+            std::lock_guard<std::mutex> lk(g_->mu);
+            g_->mailbox[{rank_, peer}].push_back(p);
+        }
+        g_->cv.notify_all();
+        t->impl = p;
+        t->live = true;
+        return SMI_SUCCESS;
+    }
+    int recv_now(void *buf, size_t bytes, int peer, hipStream_t stream) override {
+        if (peer < 0 || peer >= g_->size) {
+            set_error("recv: peer out of range");
+            return SMI_ERR_INVALID_ARG;
+        }
+        return take(buf, bytes, peer, stream);
+    }
+    int ticket_wait(SendTicket *t) override {
+        if (!t->live) return SMI_SUCCESS;
+        auto p = std::static_pointer_cast<Post>(t->impl);
+        {
+            std::unique_lock<std::mutex> lk(g_->mu);
+            g_->cv.wait(lk, [&] { return p->copied; });
+        }
+        t->live = false;
+        t->impl.reset();
+        int st = p->status;
+        SMI_HIP_CHECK(hipEventSynchronize(p->done));
+        SMI_HIP_CHECK(hipEventDestroy(p->ready));
+        SMI_HIP_CHECK(hipEventDestroy(p->done));
+        if (st != SMI_SUCCESS) set_error("local transport: peer failed to receive");
+        return st;
+    }
+
   private:
+    // Wait for the next post from `peer` (FIFO per (src, dst), like the
+    // reference's per-port FIFO order), order `stream` after the sender's
+    // `ready` event, copy, and mark the post consumed.
+    int take(void *buf, size_t bytes, int peer, hipStream_t stream) {
+        std::shared_ptr<Post> p;
+        {
+            std::unique_lock<std::mutex> lk(g_->mu);
+            auto &q = g_->mailbox[{peer, rank_}];
+            g_->cv.wait(lk, [&] { return !q.empty(); });
+            p = q.front();
+            q.pop_front();
+        }
+        int st = SMI_SUCCESS;
+        if (p->bytes != bytes) {
+            set_error("local transport: send/recv size mismatch");
+            st = SMI_ERR_COMM;
+        } else if (hipStreamWaitEvent(stream, p->ready, 0) != hipSuccess ||
+                   (bytes && hipMemcpyAsync(buf, p->buf, bytes, hipMemcpyDeviceToDevice, stream) != hipSuccess)) {
+            set_error("local transport: HIP copy failed");
+            st = SMI_ERR_HIP;
+        }
+        if (hipEventRecord(p->done, stream) != hipSuccess && st == SMI_SUCCESS) st = SMI_ERR_HIP;
+        {
+            std::lock_guard<std::mutex> lk(g_->mu);
+            p->status = st;
+            p->copied = true;
+        }
+        g_->cv.notify_all();
+        return st;
+    }
+
     struct Op {
         void *buf;
         size_t bytes;

@@ -9,7 +9,7 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DECL = re.compile(r"^\s*(?:const\s+)?(?:int|size_t|void|char)\s*\**\s*(smi_\w+)\s*\(", re.M)
+DECL = re.compile(r"^\s*(?:const\s+)?[A-Za-z_]\w*\s*\**\s*((?:smi|SMI)_\w+)\s*\(", re.M)
 
 
 def declared_symbols():
@@ -17,6 +17,7 @@ def declared_symbols():
     for h in glob.glob(os.path.join(ROOT, "include", "**", "*.h"), recursive=True):
         text = open(h).read()
         text = re.sub(r"static inline[^{]*\{[^}]*\}", "", text)  # header-only helpers
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)  # comments
         syms.update(DECL.findall(text))
     return sorted(syms)
 
@@ -30,7 +31,8 @@ def lib():
 def test_headers_declare_the_surface():
     syms = declared_symbols()
     for must in ("smi_init", "smi_finalize", "smi_stencil_run", "smi_stencil_step", "smi_reduce", "smi_bcast",
-                 "smi_gesummv", "smi_gemv_rows", "smi_reduce_fold", "smi_get_unique_id"):
+                 "smi_gesummv", "smi_gemv_rows", "smi_reduce_fold", "smi_get_unique_id", "SMI_Push", "SMI_Pop",
+                 "SMI_Open_send_channel", "SMI_Bcast", "SMI_Reduce", "SMI_Scatter", "SMI_Gather", "smi_scatter"):
         assert must in syms
 
 

@@ -1,0 +1,205 @@
+"""Element-granular channels on the GPU transport (in-process 8-rank group).
+
+Known-answer tests replayed from the reference's own suites:
+  p2p       test/p2p/p2p_rank0.cl:8-124, p2p_rank1.cl:9-175, lengths
+            {1,128,1024,10000} x receivers {1,4,7} (test/p2p/test_p2p.cpp:80-82)
+  bcast     test/broadcast/broadcast.cl:9-111, lengths {1,128,1024,10000} x
+            roots {0,4,7}
+  reduce    test/reduce/reduce.cl:7-172, lengths {1,128,300} x roots {1,4,7}
+  scatter   test/scatter/scatter.cl (root scatters i, rank r checks r*N+i)
+  gather    test/gather/gather.cl (rank r sends r; root sees 0..n-1 in order)
+plus port demultiplexing and push-before-pop buffering, and the bulk
+smi_scatter / smi_gather on device buffers.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+INT, FLOAT, DOUBLE, CHAR, SHORT = 1, 2, 3, 4, 5
+
+
+def group(n, fn):
+    from smi_amd import LocalGroup
+    return LocalGroup(n).run(fn)
+
+
+@pytest.mark.parametrize("N", [1, 128, 1024, 10000])
+@pytest.mark.parametrize("dest", [1, 4, 7])
+def test_p2p_reference_kats(gpu, N, dest):
+    from smi_amd import channels as ch
+    f1 = np.float32(1.1)
+    cases = [  # (type, port, value(i)) -- p2p_rank0.cl / p2p_rank1.cl
+        (CHAR, 1, lambda i: 3), (SHORT, 0, lambda i: 1001), (INT, 2, lambda i: i),
+        (FLOAT, 3, lambda i: np.float32(i + f1)), (DOUBLE, 4, lambda i: np.float64(i) + np.float64(f1))]
+
+    def fn(comm):
+        ok = True
+        for t, port, val in cases:
+            if comm.rank == 0:
+                c = ch.open_send_channel(N, t, dest, port, comm)
+                for i in range(N):
+                    c.push(val(i))
+            elif comm.rank == dest:
+                c = ch.open_receive_channel(N, t, 0, port, comm)
+                for i in range(N):
+                    ok &= bool(c.pop() == ch.NP[t](val(i)))
+        return ok
+
+    assert all(group(8, fn))
+
+
+def test_ports_are_separate_fifos(gpu):
+    """Interleaved pushes on two ports, popped port 1 first."""
+    from smi_amd import channels as ch
+
+    def fn(comm):
+        if comm.rank == 0:
+            a = ch.open_send_channel(300, INT, 1, 0, comm)
+            b = ch.open_send_channel(300, INT, 1, 1, comm)
+            for i in range(300):
+                a.push(i)
+                b.push(1000 + i, immediate=(i % 7 == 0))
+            return True
+        b = ch.open_receive_channel(300, INT, 0, 1, comm)
+        got_b = [b.pop() for _ in range(300)]
+        a = ch.open_receive_channel(300, INT, 0, 0, comm)
+        got_a = [a.pop() for _ in range(300)]
+        return got_a == list(range(300)) and got_b == list(range(1000, 1300))
+
+    assert all(group(2, fn))
+
+
+def test_push_before_pop_both_directions(gpu):
+    """Both ranks push 5000 floats before popping (the credit-window case)."""
+    from smi_amd import channels as ch
+
+    def fn(comm):
+        peer = 1 - comm.rank
+        s = ch.open_send_channel(5000, FLOAT, peer, 2, comm)
+        for i in range(5000):
+            s.push(np.float32(comm.rank * 10000 + i))
+        r = ch.open_receive_channel(5000, FLOAT, peer, 2, comm)
+        return all(r.pop() == np.float32(peer * 10000 + i) for i in range(5000))
+
+    assert all(group(2, fn))
+
+
+def test_transient_channel_ends_after_count(gpu):
+    from smi_amd import SMIError
+    from smi_amd import channels as ch
+
+    def fn(comm):
+        if comm.rank == 0:
+            c = ch.open_send_channel(3, INT, 1, 0, comm)
+            for i in range(3):
+                c.push(i)
+            with pytest.raises(SMIError):
+                c.push(99)
+            return True
+        c = ch.open_receive_channel(3, INT, 0, 0, comm)
+        return [c.pop() for _ in range(3)] == [0, 1, 2]
+
+    assert all(group(2, fn))
+
+
+@pytest.mark.parametrize("N", [1, 128, 1024, 10000])
+@pytest.mark.parametrize("root", [0, 4, 7])
+def test_bcast_reference_kats(gpu, N, root):
+    from smi_amd import channels as ch
+    off = np.float32(0.1)
+    cases = [(INT, 0, lambda i: i), (FLOAT, 1, lambda i: np.float32(i + off)),
+             (DOUBLE, 2, lambda i: np.float64(i) + np.float64(off)), (CHAR, 3, lambda i: root),
+             (SHORT, 4, lambda i: root)]
+
+    def fn(comm):
+        ok = True
+        for t, port, val in cases:
+            c = ch.BChannel(N, t, port, root, comm)
+            for i in range(N):
+                got = c.bcast(val(i) if comm.rank == root else 0)
+                ok &= bool(got == ch.NP[t](val(i)))
+        return ok
+
+    assert all(group(8, fn))
+
+
+@pytest.mark.parametrize("N", [1, 128, 300])
+@pytest.mark.parametrize("root", [1, 4, 7])
+def test_reduce_reference_kats(gpu, N, root):
+    from smi_amd import channels as ch
+    n = 8
+    cases = [  # (type, op, port, send(rank,i), expected(i))  -- test/reduce/reduce.cl
+        (FLOAT, 0, 0, lambda r, i: np.float32(i), lambda i: np.float32(n * i)),
+        (INT, 1, 2, lambda r, i: r + 1, lambda i: n),
+        (INT, 0, 1, lambda r, i: r + 1, lambda i: n * (n + 1) // 2),
+        (FLOAT, 2, 3, lambda r, i: np.float32(i + 0.1 * r), lambda i: np.float32(i)),
+        (DOUBLE, 0, 6, lambda r, i: np.float64(i), lambda i: np.float64(n * i)),
+        (CHAR, 1, 7, lambda r, i: r + 1, lambda i: n),
+        (SHORT, 2, 8, lambda r, i: r + 1, lambda i: 1)]
+
+    def fn(comm):
+        ok = True
+        for t, op, port, snd, exp in cases:
+            c = ch.RChannel(N, t, op, port, root, comm)
+            for i in range(N):
+                got = c.reduce(snd(comm.rank, i))
+                if comm.rank == root:
+                    ok &= bool(got == ch.NP[t](exp(i)))
+        return ok
+
+    assert all(group(n, fn))
+
+
+@pytest.mark.parametrize("N", [1, 128, 1000])
+@pytest.mark.parametrize("root", [0, 3])
+def test_scatter_gather_reference_kats(gpu, N, root):
+    from smi_amd import channels as ch
+    n = 4
+
+    def fn(comm):
+        ok = True
+        for t, port in ((INT, 0), (FLOAT, 1), (DOUBLE, 2)):
+            c = ch.ScatterChannel(N, N, t, port, root, comm)
+            bound = N * n if comm.rank == root else N
+            for i in range(bound):
+                got = c.scatter(i if comm.rank == root else 0)
+                if comm.rank != root:
+                    ok &= bool(got == ch.NP[t](comm.rank * N + i))
+                elif i // N == root:
+                    ok &= bool(got == ch.NP[t](i))  # the root's own segment
+        for t, port in ((CHAR, 3), (SHORT, 4), (INT, 5)):
+            c = ch.GatherChannel(N, N, t, port, root, comm)
+            bound = N * n if comm.rank == root else N
+            for i in range(bound):
+                got = c.gather(comm.rank)
+                if comm.rank == root:
+                    ok &= bool(got == i // N)
+        return ok
+
+    assert all(group(n, fn))
+
+
+@pytest.mark.parametrize("n", [1, 2, 8])
+def test_bulk_scatter_gather(gpu, n):
+    from smi_amd import collectives
+    count = 1000
+    root = n - 1
+    data = np.arange(n * count, dtype=np.int32) * 3
+
+    def fn(comm):
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            send = torch.from_numpy(data).cuda() if comm.rank == root else None
+            recv = torch.zeros(count, dtype=torch.int32, device="cuda")
+            collectives.scatter(comm, send, recv, root)
+            back = torch.zeros(n * count, dtype=torch.int32, device="cuda") if comm.rank == root else None
+            collectives.gather(comm, recv, back, root)
+            s.synchronize()
+            ok = np.array_equal(recv.cpu().numpy(), data[comm.rank * count:(comm.rank + 1) * count])
+            if comm.rank == root:
+                ok &= np.array_equal(back.cpu().numpy(), data)
+            return ok
+
+    assert all(group(n, fn))
