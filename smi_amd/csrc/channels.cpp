@@ -271,6 +271,21 @@ ChanState *begin_call(D *chan) {
 }
 
 }  // namespace
+
+// The last packets of a channel are detached sends: their staging slots must
+// outlive them, so finalize waits until the peers have received them.
+int channels_drain(Comm *c) {
+    if (!c->chan_engine) return SMI_SUCCESS;
+    auto *e = static_cast<ChanEngine *>(c->chan_engine.get());
+    std::lock_guard<std::mutex> lk(e->send_mu);
+    int rc = SMI_SUCCESS;
+    for (auto &t : e->tickets) {
+        const int r = c->transport->ticket_wait(&t);
+        if (rc == SMI_SUCCESS) rc = r;
+    }
+    return rc;
+}
+
 }  // namespace smi
 
 using namespace smi;

@@ -198,13 +198,14 @@ int smi_finalize(SMI_Comm comm) {
     SMI_HIP_CHECK(hipSetDevice(c->device));
     if (c->comm_stream) SMI_HIP_CHECK(hipStreamSynchronize(c->comm_stream));
     SMI_HIP_CHECK(hipDeviceSynchronize());
+    int drain_rc = channels_drain(c.get());
     c->chan_engine.reset();
     c->transport.reset();
     for (auto e : c->events) SMI_HIP_CHECK(hipEventDestroy(e));
     if (c->work) SMI_HIP_CHECK(hipFree(c->work));
     if (c->halo) SMI_HIP_CHECK(hipFree(c->halo));
     if (c->comm_stream) SMI_HIP_CHECK(hipStreamDestroy(c->comm_stream));
-    return SMI_SUCCESS;
+    return drain_rc;
 }
 
 int smi_prof_enable(int enable) {

@@ -98,6 +98,8 @@ struct Comm {
 Comm *lookup_comm(SMI_Comm c);
 int comm_workspace(Comm *c, size_t bytes, void **ptr);
 int comm_event(Comm *c, int idx, hipEvent_t *ev);
+// Wait until every detached channel send of `c` has been received (finalize).
+int channels_drain(Comm *c);
 
 // ------------------------------------------------------------ profiling --
 bool prof_enabled();
