@@ -75,8 +75,13 @@ SIGNATURES = {
 }
 
 
+def variant() -> str:
+    """SMI_LIB_VARIANT=debug selects the bounds-checked diagnostic build."""
+    return os.environ.get("SMI_LIB_VARIANT", "")
+
+
 def lib_path() -> str:
-    return _build.LIB
+    return _build.lib_path(variant())
 
 
 def load(build_if_missing: bool = True) -> ctypes.CDLL:
@@ -85,10 +90,10 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     if _lib is not None:
         return _lib
     path = lib_path()
-    if not os.path.exists(path) or (build_if_missing and _build._stale()):
+    if not os.path.exists(path) or (build_if_missing and _build._stale(variant())):
         if not build_if_missing:
             raise SMIError(f"{path} missing: run smi_amd.build.build()")
-        _build.build()
+        _build.build(variant=variant())
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in list(SIGNATURES.items()):
         fn = getattr(lib, name)

@@ -35,25 +35,36 @@ def sources() -> list[str]:
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def lib_path(variant: str = "") -> str:
+    """release: _build/libsmi_amd.so; "debug": bounds-checked diagnostic build."""
+    if variant == "debug":
+        return os.path.join(OUT_DIR, "debug", "libsmi_amd_debug.so")
+    return LIB
+
+
+def _stale(variant: str = "") -> bool:
+    lib = lib_path(variant)
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(
         os.path.join(ROOT, "include", "**", "*.h"), recursive=True)
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return LIB
-    os.makedirs(OUT_DIR, exist_ok=True)
+def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
+    lib = lib_path(variant)
+    if not force and not _stale(variant):
+        return lib
+    out_dir = os.path.dirname(lib)
+    os.makedirs(out_dir, exist_ok=True)
+    flags = CXXFLAGS + (["-DSMI_BOUNDS_CHECK"] if variant == "debug" else [])
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     objs = []
     procs = []
     for src in sources():
-        obj = os.path.join(OUT_DIR, os.path.basename(src) + ".o")
-        cmd = [hipcc, *CXXFLAGS, "-c", src, "-o", obj]
+        obj = os.path.join(out_dir, os.path.basename(src) + ".o")
+        cmd = [hipcc, *flags, "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
@@ -68,11 +79,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if failed:
         msg = "\n".join(f"--- {s}\n{o}" for s, o in failed)
         raise RuntimeError(f"hipcc failed:\n{msg}")
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     subprocess.run([hipcc, *objs, *LDFLAGS, f"--offload-arch={ARCH}", "-o", tmp], check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True,
+                variant="debug" if "--debug" in sys.argv else ""))

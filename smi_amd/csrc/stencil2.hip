@@ -15,6 +15,24 @@
 
 namespace smi {
 
+// Diagnostic builds (-DSMI_BOUNDS_CHECK, tools/debug_fused.py) check every
+// global index of the two-step kernels, record violations in a flag word and
+// clamp the access instead of faulting.  Release builds compile this away.
+#ifdef SMI_BOUNDS_CHECK
+__device__ unsigned int g_smi_oob;
+#define SMI_IDX(idx, size, code)                                   \
+    do {                                                           \
+        if ((size_t)(idx) >= (size_t)(size)) {                     \
+            atomicOr(&g_smi_oob, (unsigned)(code));                \
+            (idx) = 0;                                             \
+        }                                                          \
+    } while (0)
+#else
+#define SMI_IDX(idx, size, code) \
+    do {                         \
+    } while (0)
+#endif
+
 __device__ __forceinline__ float lane_val(float v, int lane) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
@@ -57,10 +75,14 @@ __global__ __launch_bounds__(256) void sweep2_kernel(const float *__restrict__ i
     const int ecol = last_strip ? 0 : cs + 256;
 
     auto ld = [&](int r, Row2 &R) {
-        const float *p = in + (size_t)min(max(r, 0), rows - 1) * cols;
-        R.v = *reinterpret_cast<const float4 *>(p + c0);
-        R.w = *reinterpret_cast<const float2 *>(p + wcol);
-        R.e = *reinterpret_cast<const float2 *>(p + ecol);
+        size_t base = (size_t)min(max(r, 0), rows - 1) * cols;
+        size_t iv = base + c0, iw = base + wcol, ie = base + ecol;
+        SMI_IDX(iv, (size_t)rows * cols - 3, 0x1);
+        SMI_IDX(iw, (size_t)rows * cols - 1, 0x2);
+        SMI_IDX(ie, (size_t)rows * cols - 1, 0x4);
+        R.v = *reinterpret_cast<const float4 *>(in + iv);
+        R.w = *reinterpret_cast<const float2 *>(in + iw);
+        R.e = *reinterpret_cast<const float2 *>(in + ie);
     };
     // intermediate step at row i (+ its values at columns cs-1 and cs+4nl)
     auto level1 = [&](int i, const Row2 &n, const Row2 &c, const Row2 &s, float4 &L, float &lw, float &le) {
@@ -97,7 +119,9 @@ __global__ __launch_bounds__(256) void sweep2_kernel(const float *__restrict__ i
         o.y = rcopy ? C.y : o.y;
         o.z = rcopy ? C.z : o.z;
         o.w = (rcopy || copyR) ? C.w : o.w;
-        float *op = out + (size_t)j * cols + c0;
+        size_t io = (size_t)j * cols + c0;
+        SMI_IDX(io, (size_t)rows * cols - 3, 0x8);
+        float *op = out + io;
         if (plain_store) store4<NT>(op, o);
         if (part_store) {
             if (!skipL) {
@@ -164,19 +188,38 @@ struct Ring2Ctx {
     Halo2 h;
 
     __device__ float at(int p, int q) const {  // input cell of the extended domain
-        if (p >= 0 && p < X && q >= 0 && q < Y) return in[(size_t)p * Y + q];
+        size_t i;
+        if (p >= 0 && p < X && q >= 0 && q < Y) {
+            i = (size_t)p * Y + q;
+            SMI_IDX(i, (size_t)X * Y, 0x10);
+            return in[i];
+        }
         if (p < 0) {
-            if (q >= 0 && q < Y) return h.top2 ? h.top2[(size_t)(p + 2) * Y + q] : 0.f;
+            if (q >= 0 && q < Y) {
+                i = (size_t)(p + 2) * Y + q;
+                SMI_IDX(i, 2 * (size_t)Y, 0x20);
+                return h.top2 ? h.top2[i] : 0.f;
+            }
             if (!h.corner) return 0.f;
             return q < 0 ? h.corner[0] : h.corner[1];
         }
         if (p >= X) {
-            if (q >= 0 && q < Y) return h.bot2 ? h.bot2[(size_t)(p - X) * Y + q] : 0.f;
+            if (q >= 0 && q < Y) {
+                i = (size_t)(p - X) * Y + q;
+                SMI_IDX(i, 2 * (size_t)Y, 0x40);
+                return h.bot2 ? h.bot2[i] : 0.f;
+            }
             if (!h.corner) return 0.f;
             return q < 0 ? h.corner[2] : h.corner[3];
         }
-        if (q < 0) return h.left2 ? h.left2[(size_t)(q + 2) * X + p] : 0.f;
-        return h.right2 ? h.right2[(size_t)(q - Y) * X + p] : 0.f;
+        if (q < 0) {
+            i = (size_t)(q + 2) * X + p;
+            SMI_IDX(i, 2 * (size_t)X, 0x80);
+            return h.left2 ? h.left2[i] : 0.f;
+        }
+        i = (size_t)(q - Y) * X + p;
+        SMI_IDX(i, 2 * (size_t)X, 0x100);
+        return h.right2 ? h.right2[i] : 0.f;
     }
     __device__ bool edge(int p, int q) const {
         return (p == 0 && gT) || (p == X - 1 && gB) || (q == 0 && gL) || (q == Y - 1 && gR);
@@ -206,9 +249,19 @@ __global__ __launch_bounds__(256) void ring2_kernel(Sweep2Args a, Halo2 h) {
     if (!a.skip[band] || r < 0 || r >= X || c < 0 || c >= Y) return;
     Ring2Ctx ctx{a.in, X, Y, !a.skip[0], !a.skip[1], !a.skip[2], !a.skip[3], h};
     const float v = ctx.l2(r, c);
-    a.out[(size_t)r * Y + c] = v;
-    if (h.send_left2 && c < 2) h.send_left2[(size_t)c * X + r] = v;
-    if (h.send_right2 && c >= Y - 2) h.send_right2[(size_t)(c - (Y - 2)) * X + r] = v;
+    size_t io = (size_t)r * Y + c;
+    SMI_IDX(io, (size_t)X * Y, 0x200);
+    a.out[io] = v;
+    if (h.send_left2 && c < 2) {
+        size_t i = (size_t)c * X + r;
+        SMI_IDX(i, 2 * (size_t)X, 0x400);
+        h.send_left2[i] = v;
+    }
+    if (h.send_right2 && c >= Y - 2) {
+        size_t i = (size_t)(c - (Y - 2)) * X + r;
+        SMI_IDX(i, 2 * (size_t)X, 0x800);
+        h.send_right2[i] = v;
+    }
     if (h.send_corner) {
         if (r == 0 && c == 0) h.send_corner[0] = v;
         if (r == 0 && c == Y - 1) h.send_corner[1] = v;
@@ -293,3 +346,14 @@ int launch_pack2(const float *in, int rows, int cols, const Halo2 &h, hipStream_
 }
 
 }  // namespace smi
+
+#ifdef SMI_BOUNDS_CHECK
+// Diagnostic builds only (not part of include/smi): read and clear the flags.
+extern "C" int smi_debug_oob(unsigned int *flags) {
+    SMI_HIP_CHECK(hipDeviceSynchronize());
+    SMI_HIP_CHECK(hipMemcpyFromSymbol(flags, HIP_SYMBOL(smi::g_smi_oob), sizeof(unsigned int)));
+    unsigned int zero = 0;
+    SMI_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(smi::g_smi_oob), &zero, sizeof(unsigned int)));
+    return SMI_SUCCESS;
+}
+#endif

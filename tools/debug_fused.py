@@ -2,8 +2,10 @@
 """Fused (two-step) multi-rank stencil: run cases in increasing complexity,
 one process, stop at the first failure (diagnostic)."""
 import os
+import ctypes
 import sys
 
+os.environ.setdefault("SMI_LIB_VARIANT", "debug")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -38,7 +40,12 @@ def main():
                 print(f"case {PX}x{PY} overlap={overlap} T={T} ...", flush=True)
                 got = run(g, T, PX, PY, overlap)
                 ok = np.array_equal(got.view(np.uint32), oracle.stencil(g, T).view(np.uint32))
-                print(f"   -> {'OK' if ok else 'MISMATCH'}", flush=True)
+                flags = ctypes.c_uint()
+                if os.environ.get("SMI_LIB_VARIANT") == "debug":
+                    smi_amd.load().smi_debug_oob(ctypes.byref(flags))
+                print(f"   -> {'OK' if ok else 'MISMATCH'} oob_flags=0x{flags.value:x}", flush=True)
+                if flags.value:
+                    return 2
                 if not ok:
                     bad = np.argwhere(got != oracle.stencil(g, T))
                     print("   first bad cells:", bad[:10].tolist(), flush=True)
