@@ -200,9 +200,7 @@ class LocalTransport final : public Transport {
                 rc = p->status;
             }
             SMI_HIP_CHECK(hipStreamWaitEvent(stream_, p->done, 0));
-            // destruction is deferred by the runtime until the events complete
-            SMI_HIP_CHECK(hipEventDestroy(p->ready));
-            SMI_HIP_CHECK(hipEventDestroy(p->done));
+            SMI_TRY(retire(p));
         }
         sends_.clear();
         recvs_.clear();
@@ -248,13 +246,34 @@ class LocalTransport final : public Transport {
         t->impl.reset();
         int st = p->status;
         SMI_HIP_CHECK(hipEventSynchronize(p->done));
-        SMI_HIP_CHECK(hipEventDestroy(p->ready));
-        SMI_HIP_CHECK(hipEventDestroy(p->done));
+        SMI_TRY(retire(p));
         if (st != SMI_SUCCESS) set_error("local transport: peer failed to receive");
         return st;
     }
 
+    ~LocalTransport() override {
+        // finalize has synchronised the device: no queue references them now
+        for (auto e : retired_) hipEventDestroy(e);
+    }
+
   private:
+    // A post's events may still be referenced by barrier packets that another
+    // rank's stream has not processed yet, so they are destroyed only after a
+    // device-wide synchronisation (at teardown, or when many have piled up).
+    int retire(const std::shared_ptr<Post> &p) {
+        std::lock_guard<std::mutex> lk(retire_mu_);
+        retired_.push_back(p->ready);
+        retired_.push_back(p->done);
+        if (retired_.size() >= 8192) {
+            SMI_HIP_CHECK(hipDeviceSynchronize());
+            for (auto e : retired_) SMI_HIP_CHECK(hipEventDestroy(e));
+            retired_.clear();
+        }
+        return SMI_SUCCESS;
+    }
+    std::mutex retire_mu_;
+    std::vector<hipEvent_t> retired_;
+
     // Wait for the next post from `peer` (FIFO per (src, dst), like the
     // reference's per-port FIFO order), order `stream` after the sender's
     // `ready` event, copy, and mark the post consumed.
