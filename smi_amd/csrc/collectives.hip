@@ -84,7 +84,10 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldRows rows, T *__restrict_
                 *reinterpret_cast<uint4 *>(d) = *reinterpret_cast<const uint4 *>(src);
             } else {
 #pragma unroll
-                for (int e = 0; e < VEC; ++e) d[e] = (base + e < count) ? src[e] : T(0);
+                for (int e = 0; e < VEC; ++e) {  // clamped index: safe if the load is speculated
+                    const T v = src[base + e < count ? e : (count - 1 - base)];
+                    d[e] = (base + e < count) ? v : T(0);
+                }
             }
 #pragma unroll
             for (int e = 0; e < VEC; ++e) {

@@ -59,11 +59,12 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const float *__restrict_
     for (int base = 0; base < nchunks; base += 256) {
         const int k = base + threadIdx.x;
         const bool valid = k < nchunks;
-        const float cA = valid ? chunk_dot(a, x, k) : 0.f;  // missing chunk: c = +0
+        const int kc = valid ? k : nchunks - 1;  // in-bounds even if speculated
+        const float cA = valid ? chunk_dot(a, x, kc) : 0.f;  // missing chunk: c = +0
         const float nA = dpp_from_next(cA);
         float cB = 0.f, nB = 0.f;
         if constexpr (HAS_B) {
-            cB = valid ? chunk_dot(b, x, k) : 0.f;
+            cB = valid ? chunk_dot(b, x, kc) : 0.f;
             nB = dpp_from_next(cB);
         }
         if (valid && (k & 1) == 0) {

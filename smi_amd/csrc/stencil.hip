@@ -170,11 +170,13 @@ __global__ __launch_bounds__(256) void edge_kernel(SweepArgs a, int side_mask) {
     if (copy) {
         v = in[idx];
     } else {
-        const float nv = r > 0 ? in[idx - cols] : a.halo[0][c];
-        const float sv = r < rows - 1 ? in[idx + cols] : a.halo[1][c];
-        const float wv = c > 0 ? in[idx - 1] : a.halo[2][r];
-        const float ev = c < cols - 1 ? in[idx + 1] : a.halo[3][r];
-        v = jacobi(sv, wv, ev, nv);
+        // select the address, then load once: no load of an unused halo
+        // pointer or of an out-of-tile offset can be speculated
+        const float *np = r > 0 ? in + idx - cols : a.halo[0] + c;
+        const float *sp = r < rows - 1 ? in + idx + cols : a.halo[1] + c;
+        const float *wp = c > 0 ? in + idx - 1 : a.halo[2] + r;
+        const float *ep = c < cols - 1 ? in + idx + 1 : a.halo[3] + r;
+        v = jacobi(*sp, *wp, *ep, *np);
     }
     a.out[idx] = v;
     if (c == 0 && a.send_left) a.send_left[r] = v;

@@ -187,39 +187,38 @@ struct Ring2Ctx {
     bool gT, gB, gL, gR;
     Halo2 h;
 
-    __device__ float at(int p, int q) const {  // input cell of the extended domain
+    // Input cell of the extended domain.  Every pointer of h is valid (the
+    // launcher substitutes allocated buffers for absent sides) and every
+    // index is clamped into its buffer, so the loads are safe even where the
+    // compiler executes them speculatively (it did: an unclamped negative
+    // offset from an unused NULL halo pointer faulted on gfx950).
+    __device__ float at(int p, int q) const {
+        const int pc = min(max(p, 0), X - 1), qc = min(max(q, 0), Y - 1);
         size_t i;
         if (p >= 0 && p < X && q >= 0 && q < Y) {
             i = (size_t)p * Y + q;
             SMI_IDX(i, (size_t)X * Y, 0x10);
             return in[i];
         }
-        if (p < 0) {
-            if (q >= 0 && q < Y) {
-                i = (size_t)(p + 2) * Y + q;
-                SMI_IDX(i, 2 * (size_t)Y, 0x20);
-                return h.top2 ? h.top2[i] : 0.f;
-            }
-            if (!h.corner) return 0.f;
-            return q < 0 ? h.corner[0] : h.corner[1];
+        if (p < 0 && q >= 0 && q < Y) {
+            i = (size_t)min(p + 2, 1) * Y + qc;
+            SMI_IDX(i, 2 * (size_t)Y, 0x20);
+            return h.top2[i];
         }
-        if (p >= X) {
-            if (q >= 0 && q < Y) {
-                i = (size_t)(p - X) * Y + q;
-                SMI_IDX(i, 2 * (size_t)Y, 0x40);
-                return h.bot2 ? h.bot2[i] : 0.f;
-            }
-            if (!h.corner) return 0.f;
-            return q < 0 ? h.corner[2] : h.corner[3];
+        if (p >= X && q >= 0 && q < Y) {
+            i = (size_t)min(p - X, 1) * Y + qc;
+            SMI_IDX(i, 2 * (size_t)Y, 0x40);
+            return h.bot2[i];
         }
+        if (p < 0 || p >= X) return h.corner[(p < 0 ? 0 : 2) + (q < 0 ? 0 : 1)];
         if (q < 0) {
-            i = (size_t)(q + 2) * X + p;
+            i = (size_t)min(max(q + 2, 0), 1) * X + pc;
             SMI_IDX(i, 2 * (size_t)X, 0x80);
-            return h.left2 ? h.left2[i] : 0.f;
+            return h.left2[i];
         }
-        i = (size_t)(q - Y) * X + p;
+        i = (size_t)min(max(q - Y, 0), 1) * X + pc;
         SMI_IDX(i, 2 * (size_t)X, 0x100);
-        return h.right2 ? h.right2[i] : 0.f;
+        return h.right2[i];
     }
     __device__ bool edge(int p, int q) const {
         return (p == 0 && gT) || (p == X - 1 && gB) || (q == 0 && gL) || (q == Y - 1 && gR);

@@ -45,15 +45,17 @@ static int exchange1(Comm *c, const Neighbours &nb, const float *tile, int rows,
 // side neighbour, one corner cell per diagonal neighbour.
 struct Halo2Buf {
     float *top2, *bot2, *left2, *right2, *corner, *send_left2, *send_right2, *send_corner;
-    Halo2 view(const Neighbours &nb) const {
+    // Every pointer is a valid allocation, also for sides without a
+    // neighbour (their values are never used; the kernels rely on it).
+    Halo2 view() const {
         Halo2 h;
-        h.top2 = nb.top >= 0 ? top2 : nullptr;
-        h.bot2 = nb.bottom >= 0 ? bot2 : nullptr;
-        h.left2 = nb.left >= 0 ? left2 : nullptr;
-        h.right2 = nb.right >= 0 ? right2 : nullptr;
+        h.top2 = top2;
+        h.bot2 = bot2;
+        h.left2 = left2;
+        h.right2 = right2;
         h.corner = corner;
-        h.send_left2 = nb.left >= 0 ? send_left2 : nullptr;
-        h.send_right2 = nb.right >= 0 ? send_right2 : nullptr;
+        h.send_left2 = send_left2;
+        h.send_right2 = send_right2;
         h.send_corner = send_corner;
         return h;
     }
@@ -203,7 +205,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     hb.send_left2 = hb.corner + 4;
     hb.send_right2 = hb.send_left2 + 2 * (size_t)rows;
     hb.send_corner = hb.send_right2 + 2 * (size_t)rows;
-    const Halo2 h2 = hb.view(nb);
+    const Halo2 h2 = hb.view();
     // depth-1 views: row -1, row X, col -1, col Y; packed depth-1 sends
     a.halo[0] = hb.top2 + cols;
     a.halo[1] = hb.bot2;
