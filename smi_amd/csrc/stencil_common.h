@@ -65,8 +65,8 @@ struct Tuning {
     int u = 16;         // rows in flight per batch
     int nt = 1;         // non-temporal stores
     int overlap = 1;    // overlap halo exchange with the interior sweep
-    int fuse = 1;       // Jacobi steps per pass over HBM (1 or 2)
-    int ht2 = 32;       // rows per wave (two-step sweep)
+    int fuse = 2;       // Jacobi steps per pass over HBM (1 or 2)
+    int ht2 = 8;        // rows per wave (two-step sweep)
     int u2 = 8;         // rows in flight per batch (two-step sweep)
 };
 extern Tuning g_tune;
