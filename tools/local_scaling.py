@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import smi_amd  # noqa: E402
-from smi_amd import stencil  # noqa: E402
+from smi_amd import profiling, stencil  # noqa: E402
 
 
 def run(PX, PY, n, steps, overlap):
@@ -30,7 +30,16 @@ def run(PX, PY, n, steps, overlap):
             s.synchronize()
             return time.perf_counter() - t0
 
-    return max(grp.run(fn))
+    profiling.reset()
+    profiling.enable(True)
+    t = max(grp.run(fn))
+    profiling.enable(False)
+    sw = profiling.read(profiling.SWEEP)
+    ed = profiling.read(profiling.EDGE)
+    print(json.dumps({"decomp": f"{PX}x{PY}", "overlap": overlap,
+                      "sweep_avg_ms": sw[0] / max(sw[1], 1), "sweep_n": sw[1],
+                      "edge_or_ring_avg_ms": ed[0] / max(ed[1], 1), "edge_n": ed[1]}), flush=True)
+    return t
 
 
 def main():
