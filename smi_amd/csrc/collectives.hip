@@ -77,24 +77,35 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldRows rows, T *__restrict_
         for (int e = 0; e < VEC; ++e)
 #pragma unroll
             for (int j = 0; j < S; ++j) q[e][j] = op_init<T, OP>();
-        for (int k = 0; k < n; ++k) {
-            const T *src = (const T *)rows.row[k] + base;
-            T d[VEC];
-            if (full) {
-                *reinterpret_cast<uint4 *>(d) = *reinterpret_cast<const uint4 *>(src);
-            } else {
+        // contributions in batches of KB: all loads of a batch are in flight
+        // before the (strictly ordered) fold consumes them
+        constexpr int KB = 8;
+        for (int k0 = 0; k0 < n; k0 += KB) {
+            T d[KB][VEC];
 #pragma unroll
-                for (int e = 0; e < VEC; ++e) {  // clamped index: safe if the load is speculated
-                    const T v = src[base + e < count ? e : (count - 1 - base)];
-                    d[e] = (base + e < count) ? v : T(0);
+            for (int i = 0; i < KB; ++i) {
+                const int k = min(k0 + i, n - 1);  // past n: a valid row, never folded
+                const T *src = (const T *)rows.row[k] + base;
+                if (full) {
+                    *reinterpret_cast<uint4 *>(d[i]) = *reinterpret_cast<const uint4 *>(src);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < VEC; ++e) {  // clamped index: safe if the load is speculated
+                        const T v = src[base + e < count ? e : (count - 1 - base)];
+                        d[i][e] = (base + e < count) ? v : T(0);
+                    }
                 }
             }
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) {
-                const T nv = op_apply<T, OP>(d[e], q[e][0]);
+            for (int i = 0; i < KB; ++i) {
+                if (k0 + i >= n) break;  // uniform
 #pragma unroll
-                for (int j = 0; j < S - 1; ++j) q[e][j] = q[e][j + 1];
-                q[e][S - 1] = nv;
+                for (int e = 0; e < VEC; ++e) {
+                    const T nv = op_apply<T, OP>(d[i][e], q[e][0]);
+#pragma unroll
+                    for (int j = 0; j < S - 1; ++j) q[e][j] = q[e][j + 1];
+                    q[e][S - 1] = nv;
+                }
             }
         }
         T r[VEC];

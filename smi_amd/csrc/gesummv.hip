@@ -11,9 +11,14 @@
 // MI355X design: the functional split (A on rank 0, B on rank 1) becomes a
 // row split over all ranks -- each rank owns contiguous rows of both A and B
 // and computes both terms locally, so only the y chunks travel (to the root).
-// One workgroup per row: every lane owns one 64-element chunk and forms c_k
-// in the reference order; lane pairs form the tile sums through DPP; the
-// strictly sequential row fold runs in one lane per matrix.
+//
+// One wave per row (A and B).  The row is walked in slabs of 64 chunks
+// (16 KiB): the wave reads a slab with fully coalesced float4 loads, forms
+// the products a*x in that layout, and transposes them through LDS so that
+// lane l holds chunk l and sums its 64 products sequentially (the reference
+// order).  Lane pairs form the tile sums through DPP, and the sequential row
+// fold consumes the slab's tiles in order from lane 0 (readlane), so no tile
+// array is kept and m is unbounded.
 #include <algorithm>
 
 #include "smi_internal.h"
@@ -25,81 +30,101 @@ __device__ __forceinline__ float dpp_from_next(float v) {  // lane i <- lane i+1
         float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
 }
 
-// c_k for chunk k of row `a` (64 products, summed sequentially from 0).
-__device__ __forceinline__ float chunk_dot(const float *__restrict__ a, const float *__restrict__ x, int k) {
-    const float4 *ap = reinterpret_cast<const float4 *>(a + 64 * (size_t)k);
-    const float4 *xp = reinterpret_cast<const float4 *>(x + 64 * (size_t)k);
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const float4 av = ap[j], xv = xp[j];
-        acc = __fadd_rn(acc, __fmul_rn(av.x, xv.x));
-        acc = __fadd_rn(acc, __fmul_rn(av.y, xv.y));
-        acc = __fadd_rn(acc, __fmul_rn(av.z, xv.z));
-        acc = __fadd_rn(acc, __fmul_rn(av.w, xv.w));
-    }
-    return acc;
+__device__ __forceinline__ float4 mul4(float4 a, float4 b) {
+    return make_float4(__fmul_rn(a.x, b.x), __fmul_rn(a.y, b.y), __fmul_rn(a.z, b.z), __fmul_rn(a.w, b.w));
 }
 
-// One block per row.  LDS holds the per-tile sums of A (and B).
+// LDS between the writes and reads of other lanes of the same wave
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int kGemvWaves = 4;
+constexpr int kSlabStride = 17;  // float4s per chunk in LDS (64 floats + 4 pad: conflict-free)
+
+// c for the chunk this lane owns: products of slab `pv` (coalesced layout:
+// pv[j] = elements 4*(64j + lane) .. +3 of the slab) transposed through `wb`.
+__device__ __forceinline__ float chunk_sum(float4 *wb, const float4 (&pv)[16], int lane) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) wb[(4 * j + (lane >> 4)) * kSlabStride + (lane & 15)] = pv[j];
+    wave_lds_sync();
+    float c = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const float4 p = wb[lane * kSlabStride + q];
+        c = __fadd_rn(c, p.x);
+        c = __fadd_rn(c, p.y);
+        c = __fadd_rn(c, p.z);
+        c = __fadd_rn(c, p.w);
+    }
+    wave_lds_sync();  // reads done before the next slab overwrites
+    return c;
+}
+
 template <bool HAS_B>
-__global__ __launch_bounds__(256) void gemv_rows_kernel(const float *__restrict__ A,
-                                                        const float *__restrict__ B,
-                                                        const float *__restrict__ x, float *__restrict__ y,
-                                                        int m, int lda, float alpha, float beta) {
-    extern __shared__ __attribute__((aligned(16))) float tiles[];
-    const int row = blockIdx.x;
-    const int nchunks = m / 64;
-    const int ntiles = (nchunks + 1) / 2;
-    float *tA = tiles;
-    float *tB = tiles + ntiles;
+__global__ __launch_bounds__(64 * kGemvWaves) void gemv_rows_kernel(const float *__restrict__ A,
+                                                                   const float *__restrict__ B,
+                                                                   const float *__restrict__ x,
+                                                                   float *__restrict__ y, int n, int m, int lda,
+                                                                   float alpha, float beta) {
+    __shared__ float4 lds[kGemvWaves][64 * kSlabStride];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * kGemvWaves + wave;
+    if (row >= n) return;  // wave-uniform; the kernel has no block barrier
+    float4 *wb = lds[wave];
+    const int nchunks = m >> 6;
     const float *a = A + (size_t)row * lda;
-    const float *b = HAS_B ? B + (size_t)row * lda : nullptr;
-    // Rounds of 256 chunks; every lane of the block takes part in the DPP.
-    for (int base = 0; base < nchunks; base += 256) {
-        const int k = base + threadIdx.x;
-        const bool valid = k < nchunks;
-        const int kc = valid ? k : nchunks - 1;  // in-bounds even if speculated
-        const float cA = valid ? chunk_dot(a, x, kc) : 0.f;  // missing chunk: c = +0
+    const float *b = HAS_B ? B + (size_t)row * lda : a;
+    float accA = 0.f, accB = 0.f;
+    for (int cbase = 0; cbase < nchunks; cbase += 64) {
+        float4 pa[16], pb[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int ch = min(cbase + 4 * j + (lane >> 4), nchunks - 1);  // clamped: the tail
+            const int e = ch * 64 + (lane & 15) * 4;                       // chunk's c is replaced
+            const float4 xv = *reinterpret_cast<const float4 *>(x + e);
+            pa[j] = mul4(*reinterpret_cast<const float4 *>(a + e), xv);
+            if constexpr (HAS_B) pb[j] = mul4(*reinterpret_cast<const float4 *>(b + e), xv);
+        }
+        const bool valid = cbase + lane < nchunks;
+        // every lane writes slots of other lanes' chunks: transpose on all
+        // lanes, then replace a missing chunk's c by +0
+        float cA = chunk_sum(wb, pa, lane);
+        cA = valid ? cA : 0.f;
         const float nA = dpp_from_next(cA);
-        float cB = 0.f, nB = 0.f;
+        const float tA = __fadd_rn(__fadd_rn(0.f, __fmul_rn(alpha, cA)), __fmul_rn(alpha, nA));
+        float tB = 0.f;
         if constexpr (HAS_B) {
-            cB = valid ? chunk_dot(b, x, kc) : 0.f;
-            nB = dpp_from_next(cB);
+            float cB = chunk_sum(wb, pb, lane);
+            cB = valid ? cB : 0.f;
+            const float nB = dpp_from_next(cB);
+            tB = __fadd_rn(__fadd_rn(0.f, __fmul_rn(beta, cB)), __fmul_rn(beta, nB));
         }
-        if (valid && (k & 1) == 0) {
-            const int t = k >> 1;
-            tA[t] = __fadd_rn(__fadd_rn(0.f, __fmul_rn(alpha, cA)), __fmul_rn(alpha, nA));
+        // tiles of this slab live in the even lanes, in order
+        const int ntl = min(32, (nchunks - cbase + 1) >> 1);
+        for (int k = 0; k < ntl; ++k) {
+            accA = __fadd_rn(accA, __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                                                 __builtin_bit_cast(int, tA), 2 * k)));
             if constexpr (HAS_B)
-                tB[t] = __fadd_rn(__fadd_rn(0.f, __fmul_rn(beta, cB)), __fmul_rn(beta, nB));
+                accB = __fadd_rn(accB, __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                                                     __builtin_bit_cast(int, tB), 2 * k)));
         }
     }
-    __syncthreads();
-    // sequential row folds: lane 0 folds A, lane 64 (next wave) folds B
-    if (threadIdx.x == 0 || (HAS_B && threadIdx.x == 64)) {
-        const float *t = threadIdx.x == 0 ? tA : tB;
-        float acc = 0.f;
-        for (int i = 0; i < ntiles; ++i) acc = __fadd_rn(acc, t[i]);
-        if (threadIdx.x == 64) tB[0] = acc;  // hand yB to lane 0 (tB[0] already consumed)
-        else tA[0] = acc;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) y[row] = HAS_B ? __fadd_rn(tA[0], tB[0]) : tA[0];
+    if (lane == 0) y[row] = HAS_B ? __fadd_rn(accA, accB) : accA;
 }
 
 static int launch_gemv(const float *A, const float *B, const float *x, float *y, int n, int m, int lda,
                        float alpha, float beta, hipStream_t s) {
     if (n == 0) return SMI_SUCCESS;
-    const int ntiles = (m / 64 + 1) / 2;
-    const size_t lds = (size_t)2 * std::max(ntiles, 1) * sizeof(float);
-    SMI_ARG_CHECK(lds <= 64 * 1024, "m too large for one row per workgroup");
     int tok = -1;
     if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_GEMV, s, &tok));
+    const dim3 grid((n + kGemvWaves - 1) / kGemvWaves), block(64 * kGemvWaves);
     if (B)
-        hipLaunchKernelGGL(gemv_rows_kernel<true>, dim3(n), dim3(256), lds, s, A, B, x, y, m, lda, alpha, beta);
+        hipLaunchKernelGGL(gemv_rows_kernel<true>, grid, block, 0, s, A, B, x, y, n, m, lda, alpha, beta);
     else
-        hipLaunchKernelGGL(gemv_rows_kernel<false>, dim3(n), dim3(256), lds, s, A, B, x, y, m, lda, alpha,
-                           beta);
+        hipLaunchKernelGGL(gemv_rows_kernel<false>, grid, block, 0, s, A, B, x, y, n, m, lda, alpha, beta);
     SMI_HIP_CHECK(hipGetLastError());
     if (tok >= 0) SMI_TRY(prof_end(tok, s));
     return SMI_SUCCESS;

@@ -12,7 +12,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("shape", [(1, 64), (5, 128), (17, 192), (128, 1024), (64, 4096), (3, 33 * 64)])
+# m spans: one chunk, odd chunk counts (a lone last tile), slab (64-chunk)
+# boundaries +-1, several full slabs
+@pytest.mark.parametrize("shape", [(1, 64), (5, 128), (17, 192), (128, 1024), (64, 4096), (3, 33 * 64),
+                                   (7, 65 * 64), (9, 127 * 64), (4, 129 * 64), (6, 3 * 64 * 64)])
 def test_gemv_rows_matches_oracle(gpu, oracle_mod, shape):
     from smi_amd import gesummv
     n, m = shape
@@ -24,6 +27,23 @@ def test_gemv_rows_matches_oracle(gpu, oracle_mod, shape):
     got = gesummv.gemv_rows(torch.from_numpy(A).cuda(), torch.from_numpy(B).cuda(),
                             torch.from_numpy(x).cuda(), 1.5, 0.5).cpu().numpy()
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_gemv_rows_strided_and_single_matrix(gpu, oracle_mod):
+    """lda > m (a column window of a wider matrix) and the A-only form
+    (rank 0 of the reference with beta = 0, gesummv_smi.cpp:224)."""
+    from smi_amd import gesummv
+    n, m, lda = 13, 130 * 64, 130 * 64 + 4
+    rng = np.random.default_rng(5)
+    W = rng.random((n, lda), dtype=np.float32) * 2 - 1
+    x = rng.random(m, dtype=np.float32) * 2 - 1
+    A = torch.from_numpy(W).cuda()[:, :m]
+    got = gesummv.gemv_rows(A, A, torch.from_numpy(x).cuda(), 1.25, -0.75).cpu().numpy()
+    want = oracle_mod.gesummv(W[:, :m], W[:, :m], x, 1.25, -0.75)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    got1 = gesummv.gemv_rows(A, None, torch.from_numpy(x).cuda(), 1.25, 0.0).cpu().numpy()
+    want1 = oracle_mod.gesummv(W[:, :m], np.zeros((n, m), np.float32), x, 1.25, 0.0)
+    assert np.array_equal(got1, want1)
 
 
 def test_reference_pattern(gpu, oracle_mod):
