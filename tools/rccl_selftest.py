@@ -20,6 +20,13 @@ from smi_amd import collectives, gesummv, stencil  # noqa: E402
 
 def main():
     rank = int(os.environ["RANK"])
+    if os.environ.get("SMI_FAKE_HOSTS") == "1":
+        # One GPU, several ranks: RCCL refuses two ranks on one device of one
+        # host ("Duplicate GPU detected"), so give every rank its own host id;
+        # RCCL then moves the bytes over its socket transport on loopback.
+        os.environ["NCCL_HOSTID"] = f"smi-selftest-host-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     world = int(os.environ["WORLD_SIZE"])
     dev = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
     torch.cuda.set_device(dev)
@@ -50,22 +57,26 @@ def main():
         good = np.array_equal(buf.cpu().numpy(), data)
         print(f"[{rank}] bcast: {'OK' if good else 'MISMATCH'}", flush=True)
         ok &= good
-        # decomposed stencil 1 x world
-        PX, PY = 1, world
-        g = oracle.init_uniform(256, 256 * world, seed=5)
+        # decomposed stencil (1 x world, or 2 x world/2)
+        PX, PY = (2, world // 2) if world % 2 == 0 and world >= 4 else (1, world)
+        g = oracle.init_uniform(256 * PX, 256 * PY, seed=5)
         tiles = stencil.split_memory(g, PX, PY)
         t = torch.from_numpy(tiles[rank]).cuda()
+        want = oracle.stencil(g, 13) if rank == 0 else None
         for overlap in (1, 0):
-            stencil.set_tuning(overlap=overlap)
-            res = stencil.run(comm, t.clone(), 12, PX, PY)
-            s.synchronize()
-            tiles_out = [None] * world
-            dist.all_gather_object(tiles_out, res.cpu().numpy())
-            if rank == 0:
-                got = stencil.combine_memory(tiles_out, PX, PY)
-                good = np.array_equal(got.view(np.uint32), oracle.stencil(g, 12).view(np.uint32))
-                print(f"[0] stencil 1x{world} overlap={overlap}: {'OK' if good else 'MISMATCH'}", flush=True)
-                ok &= good
+            for fuse in (1, 2):
+                stencil.set_tuning(overlap=overlap)
+                stencil.set_fusion(steps_per_pass=fuse)
+                res = stencil.run(comm, t.clone(), 13, PX, PY)
+                s.synchronize()
+                tiles_out = [None] * world
+                dist.all_gather_object(tiles_out, res.cpu().numpy())
+                if rank == 0:
+                    got = stencil.combine_memory(tiles_out, PX, PY)
+                    good = np.array_equal(got.view(np.uint32), want.view(np.uint32))
+                    print(f"[0] stencil {PX}x{PY} overlap={overlap} fuse={fuse}: "
+                          f"{'OK' if good else 'MISMATCH'}", flush=True)
+                    ok &= good
         # gesummv
         n, m = 1000, 1024
         rng = np.random.default_rng(7)
