@@ -74,7 +74,11 @@ int comm_event(Comm *c, int idx, hipEvent_t *ev) {
 }
 
 static int finish_init(std::unique_ptr<Comm> c, SMI_Comm *out) {
-    SMI_HIP_CHECK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    // highest priority: the ring kernels and the exchange it carries are on
+    // the critical path, the interior sweep beside them is not
+    int least = 0, greatest = 0;
+    SMI_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    SMI_HIP_CHECK(hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, greatest));
     return register_comm(std::move(c), out);
 }
 

@@ -68,6 +68,8 @@ struct Tuning {
     int fuse = 2;       // Jacobi steps per pass over HBM (1 or 2)
     int ht2 = 8;        // rows per wave (two-step sweep)
     int u2 = 8;         // rows in flight per batch (two-step sweep)
+    int htk = 32;       // rows per wave (K-step sweep, K >= 4)
+    int uk = 8;         // rows in flight per batch (K-step sweep)
 };
 extern Tuning g_tune;
 
@@ -98,5 +100,47 @@ struct Halo2 {
 int launch_sweep2(const Sweep2Args &a, hipStream_t s);
 int launch_ring2(const Sweep2Args &a, const Halo2 &h, hipStream_t s);
 int launch_pack2(const float *in, int rows, int cols, const Halo2 &h, hipStream_t s);
+
+// K steps per pass (stencilk.hip, K = 4 or 8): output rectangle
+// [row_lo,row_hi) x [col_lo,col_hi) of the tile, computed from input cells
+// within K of it (all inside the tile); g* = 1 where the side is a global
+// edge of the grid (its outermost row/column is copied every step).
+struct SweepKArgs {
+    const float *in;
+    float *out;
+    int rows, cols;
+    int row_lo, row_hi, col_lo, col_hi;
+    int gT, gB, gL, gR;
+};
+int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s);
+
+// Depth-K halos (stencil_ringk.hip).  Receive side: top = rows -K..-1 and
+// bot = rows X..X+K-1 (K x Y, row-major), left = cols -K..-1 and right =
+// cols Y..Y+K-1 (X x K, [row][k]), corner[tl,tr,bl,br] = K x K blocks of the
+// diagonal neighbours.  Send side: send_left/right = this tile's cols 0..K-1
+// / Y-K..Y-1 ([row][k]), send_corner = its own four K x K corner blocks.
+// The top/bottom rows are sent straight from the tile.  Every pointer is a
+// valid allocation, also for sides without a neighbour.
+struct HaloK {
+    const float *top, *bot, *left, *right;
+    const float *corner[4];
+    float *send_left, *send_right;
+    float *send_corner[4];
+};
+constexpr int RB_H = 64;  // ring block rows (left/right bands)
+constexpr int RB_W = 64;  // ring block columns (top/bottom bands)
+struct RingKArgs {
+    const float *in;
+    float *out;
+    int rows, cols, k;
+    int has[4];        // neighbour on side top, bottom, left, right
+    int has_diag[4];   // neighbour tl, tr, bl, br
+    HaloK h;
+    // filled by launch_ringk: band rectangles and block prefix
+    int r0[4], r1[4], c0[4], c1[4];
+    int first_block[5];
+};
+int launch_ringk(RingKArgs a, hipStream_t s);
+int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s);
 
 }  // namespace smi

@@ -1,0 +1,161 @@
+// stencil_ringk.hip -- the halo-facing ring of a K-step pass (K = 4, 8).
+//
+// In a multi-rank run with K Jacobi steps per pass, every tile cell within K
+// of a side that has a neighbour depends on that neighbour's cells (up to K
+// rows/columns deep, plus a K x K block from each diagonal neighbour for the
+// corners).  The ring kernel computes exactly those cells: the ring is cut
+// into small output blocks; each workgroup loads its block plus a K-cell
+// apron from the "extended tile" (tile cells, depth-K halos, corner blocks)
+// into LDS, runs the K levels in LDS (the valid region shrinks by one cell
+// per level), stores the block, and packs the new left/right columns and
+// corner blocks for the next exchange.  The per-cell arithmetic and the
+// global-edge copy rule are the sweep's (stencil_smi.cl:143-156); cells of
+// the apron that lie outside the global grid are never used by a stored cell.
+#include "stencil_common.h"
+
+namespace smi {
+
+// extended-tile cell (p, q), p in [-K, X+K), q in [-K, Y+K); 0 where no data
+// exists (outside the global grid: only ever read by unused cells)
+__device__ __forceinline__ float ext_at(const RingKArgs &a, int p, int q) {
+    const int X = a.rows, Y = a.cols, K = a.k;
+    const bool pin = p >= 0 && p < X, qin = q >= 0 && q < Y;
+    // every index is clamped into its buffer, so a load the compiler
+    // executes ahead of its branch can never leave the allocation
+    const int pc = min(max(p, 0), X - 1), qc = min(max(q, 0), Y - 1);
+    if (pin && qin) return a.in[(size_t)pc * Y + qc];
+    if (qin) {
+        if (p < 0) return a.has[0] ? a.h.top[(size_t)max(p + K, 0) * Y + qc] : 0.f;
+        return a.has[1] ? a.h.bot[(size_t)min(p - X, K - 1) * Y + qc] : 0.f;
+    }
+    if (pin) {
+        if (q < 0) return a.has[2] ? a.h.left[(size_t)pc * K + max(q + K, 0)] : 0.f;
+        return a.has[3] ? a.h.right[(size_t)pc * K + min(q - Y, K - 1)] : 0.f;
+    }
+    const int ci = (p < 0 ? 0 : 2) + (q < 0 ? 0 : 1);  // tl, tr, bl, br
+    if (!a.has_diag[ci]) return 0.f;
+    const int i = min(max(p < 0 ? p + K : p - X, 0), K - 1);
+    const int j = min(max(q < 0 ? q + K : q - Y, 0), K - 1);
+    return a.h.corner[ci][i * K + j];
+}
+
+// Output blocks: top/bottom bands in K x RB_W blocks, left/right bands in
+// RB_H x K blocks (block b -> band via the prefix table in RingKArgs).
+template <int K>
+__global__ __launch_bounds__(256) void ringk_kernel(RingKArgs a) {
+    // horizontal blocks: 3K x (RB_W + 2K); vertical blocks: (RB_H + 2K) x 3K
+    constexpr int LDS_N = 3 * K * ((RB_W > RB_H ? RB_W : RB_H) + 2 * K);
+    __shared__ float lds[2][LDS_N];
+    const int b = blockIdx.x;
+    int band = 0;
+    while (band < 3 && b >= a.first_block[band + 1]) ++band;
+    const int lb = b - a.first_block[band];
+    const int r0 = a.r0[band], r1 = a.r1[band], c0 = a.c0[band], c1 = a.c1[band];
+    const bool horiz = band < 2;  // top/bottom band: K rows x wide
+    const int bh = horiz ? K : RB_H, bw = horiz ? RB_W : K;
+    const int nbc = (c1 - c0 + bw - 1) / bw;
+    const int oR0 = r0 + (lb / nbc) * bh, oC0 = c0 + (lb % nbc) * bw;
+    const int oR1 = min(oR0 + bh, r1), oC1 = min(oC0 + bw, c1);
+    const int H = oR1 - oR0 + 2 * K, W = oC1 - oC0 + 2 * K;
+    const int pb = oR0 - K, qb = oC0 - K;  // extended coordinates of lds (0,0)
+    const int X = a.rows, Y = a.cols;
+    const bool gT = !a.has[0], gB = !a.has[1], gL = !a.has[2], gR = !a.has[3];
+
+    for (int i = threadIdx.x; i < H * W; i += 256) {
+        const int y = i / W, x = i - y * W;
+        lds[0][i] = ext_at(a, pb + y, qb + x);
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int l = 1; l <= K; ++l) {
+        const float *src = lds[(l - 1) & 1];
+        float *dst = lds[l & 1];
+        const int hl = H - 2 * l, wl = W - 2 * l;
+        for (int i = threadIdx.x; i < hl * wl; i += 256) {
+            const int y = l + i / wl, x = l + i % wl;
+            const int p = pb + y, q = qb + x;
+            const int o = y * W + x;
+            const bool copy = (p == 0 && gT) || (p == X - 1 && gB) || (q == 0 && gL) || (q == Y - 1 && gR);
+            dst[o] = copy ? src[o] : jacobi(src[o + W], src[o - 1], src[o + 1], src[o - W]);
+        }
+        __syncthreads();
+    }
+    const float *res = lds[K & 1];
+    const int oh = oR1 - oR0, ow = oC1 - oC0;
+    for (int i = threadIdx.x; i < oh * ow; i += 256) {
+        const int y = i / ow, x = i - y * ow;
+        const int p = oR0 + y, q = oC0 + x;
+        const float v = res[(y + K) * W + (x + K)];
+        a.out[(size_t)p * Y + q] = v;
+        if (q < K) a.h.send_left[(size_t)p * K + q] = v;
+        if (q >= Y - K) a.h.send_right[(size_t)p * K + (q - (Y - K))] = v;
+        if (p < K || p >= X - K) {
+            const int pi = p < K ? p : p - (X - K);
+            if (q < K) a.h.send_corner[p < K ? 0 : 2][pi * K + q] = v;
+            if (q >= Y - K) a.h.send_corner[p < K ? 1 : 3][pi * K + (q - (Y - K))] = v;
+        }
+    }
+}
+
+// Initial depth-K sends from the current tile: columns 0..K-1 and Y-K..Y-1
+// packed [row][k], and the four K x K corner blocks.
+__global__ __launch_bounds__(256) void packk_kernel(const float *in, int X, int Y, int K, HaloK h) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= X * K) return;
+    const int p = t / K, k = t - p * K;
+    const float *row = in + (size_t)p * Y;
+    const float vl = row[k], vr = row[Y - K + k];
+    h.send_left[t] = vl;
+    h.send_right[t] = vr;
+    if (p < K) {
+        h.send_corner[0][p * K + k] = vl;
+        h.send_corner[1][p * K + k] = vr;
+    }
+    if (p >= X - K) {
+        h.send_corner[2][(p - (X - K)) * K + k] = vl;
+        h.send_corner[3][(p - (X - K)) * K + k] = vr;
+    }
+}
+
+int launch_ringk(RingKArgs a, hipStream_t s) {
+    const int X = a.rows, Y = a.cols, K = a.k;
+    SMI_ARG_CHECK(K == 4 || K == 8, "ring: K must be 4 or 8");
+    SMI_ARG_CHECK(X >= 2 * K && Y >= 2 * K, "ring: tile smaller than 2K");
+    // bands: top rows [0,K), bottom rows [X-K,X) (full width); left/right
+    // columns over the rows the top/bottom bands leave
+    const int rlo = a.has[0] ? K : 0, rhi = a.has[1] ? X - K : X;
+    const int band_r0[4] = {0, X - K, rlo, rlo}, band_r1[4] = {K, X, rhi, rhi};
+    const int band_c0[4] = {0, 0, 0, Y - K}, band_c1[4] = {Y, Y, K, Y};
+    int nb = 0;
+    for (int k = 0; k < 4; ++k) {
+        a.r0[k] = band_r0[k];
+        a.r1[k] = band_r1[k];
+        a.c0[k] = band_c0[k];
+        a.c1[k] = band_c1[k];
+        a.first_block[k] = nb;
+        if (!a.has[k] || a.r1[k] <= a.r0[k]) continue;
+        const bool horiz = k < 2;
+        const int bh = horiz ? K : RB_H, bw = horiz ? RB_W : K;
+        nb += ((a.r1[k] - a.r0[k] + bh - 1) / bh) * ((a.c1[k] - a.c0[k] + bw - 1) / bw);
+    }
+    a.first_block[4] = nb;
+    if (nb == 0) return SMI_SUCCESS;
+    int tok = -1;
+    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_EDGE, s, &tok));
+    if (K == 4)
+        hipLaunchKernelGGL(ringk_kernel<4>, dim3(nb), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(ringk_kernel<8>, dim3(nb), dim3(256), 0, s, a);
+    SMI_HIP_CHECK(hipGetLastError());
+    if (tok >= 0) SMI_TRY(prof_end(tok, s));
+    return SMI_SUCCESS;
+}
+
+int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s) {
+    const int n = rows * K;
+    hipLaunchKernelGGL(packk_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, rows, cols, K, h);
+    SMI_HIP_CHECK(hipGetLastError());
+    return SMI_SUCCESS;
+}
+
+}  // namespace smi

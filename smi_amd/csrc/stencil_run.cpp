@@ -91,6 +91,58 @@ static int exchange2(Comm *c, const Neighbours &nb, const float *tile, int rows,
     return tp->end();
 }
 
+// Depth-K exchange (once per K steps): K rows / K columns per side
+// neighbour, one K x K block per diagonal neighbour.
+struct HaloKBuf {
+    float *top, *bot, *left, *right, *send_left, *send_right;
+    float *corner[4], *send_corner[4];
+    HaloK view() const {
+        HaloK h;
+        h.top = top;
+        h.bot = bot;
+        h.left = left;
+        h.right = right;
+        h.send_left = send_left;
+        h.send_right = send_right;
+        for (int k = 0; k < 4; ++k) {
+            h.corner[k] = corner[k];
+            h.send_corner[k] = send_corner[k];
+        }
+        return h;
+    }
+};
+
+static int exchangek(Comm *c, const Neighbours &nb, const float *tile, int rows, int cols, int K, const HaloKBuf &h,
+                     hipStream_t s) {
+    Transport *tp = c->transport.get();
+    const size_t rb = (size_t)K * cols * sizeof(float), cb = (size_t)rows * K * sizeof(float);
+    const size_t kb = (size_t)K * K * sizeof(float);
+    SMI_TRY(tp->begin(s));
+    if (nb.top >= 0) {
+        SMI_TRY(tp->send(tile, rb, nb.top));
+        SMI_TRY(tp->recv(h.top, rb, nb.top));
+    }
+    if (nb.bottom >= 0) {
+        SMI_TRY(tp->send(tile + (size_t)(rows - K) * cols, rb, nb.bottom));
+        SMI_TRY(tp->recv(h.bot, rb, nb.bottom));
+    }
+    if (nb.left >= 0) {
+        SMI_TRY(tp->send(h.send_left, cb, nb.left));
+        SMI_TRY(tp->recv(h.left, cb, nb.left));
+    }
+    if (nb.right >= 0) {
+        SMI_TRY(tp->send(h.send_right, cb, nb.right));
+        SMI_TRY(tp->recv(h.right, cb, nb.right));
+    }
+    const int diag[4] = {nb.tl, nb.tr, nb.bl, nb.br};
+    for (int k = 0; k < 4; ++k) {
+        if (diag[k] < 0) continue;
+        SMI_TRY(tp->send(h.send_corner[k], kb, diag[k]));
+        SMI_TRY(tp->recv(h.corner[k], kb, diag[k]));
+    }
+    return tp->end();
+}
+
 static int ensure_halo(Comm *c, size_t elems) {
     if (c->halo_elems < elems) {
         if (c->halo) SMI_HIP_CHECK(hipFree(c->halo));
@@ -109,22 +161,26 @@ extern "C" {
 
 int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_flight) {
     if (steps_per_pass > 0) {
-        SMI_ARG_CHECK(steps_per_pass == 1 || steps_per_pass == 2, "steps_per_pass must be 1 or 2");
+        SMI_ARG_CHECK(steps_per_pass == 1 || steps_per_pass == 2 || steps_per_pass == 4 || steps_per_pass == 8,
+                      "steps_per_pass must be 1, 2, 4 or 8");
         g_tune.fuse = steps_per_pass;
     }
-    if (rows_per_wave > 0) g_tune.ht2 = rows_per_wave;
+    // rows_per_wave / rows_in_flight tune the kernel of the current setting
+    const bool deep = g_tune.fuse >= 4;
+    if (rows_per_wave > 0) (deep ? g_tune.htk : g_tune.ht2) = rows_per_wave;
     if (rows_in_flight > 0) {
         SMI_ARG_CHECK(rows_in_flight == 1 || rows_in_flight == 2 || rows_in_flight == 4 || rows_in_flight == 8,
                       "rows_in_flight must be 1, 2, 4 or 8");
-        g_tune.u2 = rows_in_flight;
+        (deep ? g_tune.uk : g_tune.u2) = rows_in_flight;
     }
     return SMI_SUCCESS;
 }
 
 int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in_flight) {
+    const bool deep = g_tune.fuse >= 4;
     if (steps_per_pass) *steps_per_pass = g_tune.fuse;
-    if (rows_per_wave) *rows_per_wave = g_tune.ht2;
-    if (rows_in_flight) *rows_in_flight = g_tune.u2;
+    if (rows_per_wave) *rows_per_wave = deep ? g_tune.htk : g_tune.ht2;
+    if (rows_in_flight) *rows_in_flight = deep ? g_tune.uk : g_tune.u2;
     return SMI_SUCCESS;
 }
 
@@ -158,10 +214,17 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     for (int k = 0; k < 4; ++k)
         if (side_nb[k] >= 0) side_mask |= 1 << k;
 
-    const bool fused = g_tune.fuse == 2 && rows >= 4 && cols >= 8;
-    const int pairs = fused ? timesteps / 2 : 0;
-    const int singles = timesteps - 2 * pairs;
-    *result_index = (pairs + singles) & 1;
+    // K steps per pass for the bulk (tiles of at least 2K x 2K when
+    // multi-rank), then pairs of steps, then single steps
+    int K = g_tune.fuse >= 4 ? g_tune.fuse : 0;
+    if (K && side_mask && (rows < 2 * K || cols < 2 * K)) K = 0;
+    if (K && cols < 8) K = 0;
+    const int kpasses = K ? timesteps / K : 0;
+    const int rest = timesteps - K * kpasses;
+    const bool fused = g_tune.fuse >= 2 && rows >= 4 && cols >= 8;
+    const int pairs = fused ? rest / 2 : 0;
+    const int singles = rest - 2 * pairs;
+    *result_index = (kpasses + pairs + singles) & 1;
     if (timesteps == 0) return SMI_SUCCESS;
 
     // single-step arguments (modes / halo views set below)
@@ -173,11 +236,28 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     a2.rows = rows;
     a2.cols = cols;
     for (int k = 0; k < 4; ++k) a2.skip[k] = side_nb[k] >= 0;
+    // K-step interior: stays K cells clear of every halo-facing side
+    SweepKArgs ak{};
+    ak.rows = rows;
+    ak.cols = cols;
+    ak.row_lo = nb.top >= 0 ? K : 0;
+    ak.row_hi = nb.bottom >= 0 ? rows - K : rows;
+    ak.col_lo = nb.left >= 0 ? K : 0;
+    ak.col_hi = nb.right >= 0 ? cols - K : cols;
+    ak.gT = nb.top < 0;
+    ak.gB = nb.bottom < 0;
+    ak.gL = nb.left < 0;
+    ak.gR = nb.right < 0;
 
     int cur = 0;  // index of the buffer holding the current state
     auto bufp = [&](int i) { return i ? buf1 : buf0; };
 
     if (side_mask == 0) {  // single tile: no halos, no exchange
+        for (int p = 0; p < kpasses; ++p, cur ^= 1) {
+            ak.in = bufp(cur);
+            ak.out = bufp(cur ^ 1);
+            SMI_TRY(launch_sweepk(K, ak, s));
+        }
         for (int p = 0; p < pairs; ++p, cur ^= 1) {
             a2.in = bufp(cur);
             a2.out = bufp(cur ^ 1);
@@ -191,11 +271,13 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
         return SMI_SUCCESS;
     }
 
-    // Halo staging.  Depth 2 (used by both modes; the depth-1 views are its
-    // inner row/column): top2 | bot2 | left2 | right2 | corner(4) |
-    // send_left2 | send_right2 | send_corner(4).
-    const size_t need = 4 * (size_t)cols + 8 * (size_t)rows + 8;
-    SMI_TRY(ensure_halo(c, need));
+    // Halo staging.  Depth 2 (its inner row/column doubles as the depth-1
+    // halo): top2 | bot2 | left2 | right2 | corner(4) | send_left2 |
+    // send_right2 | send_corner(4); then depth K: top | bot (K x cols) |
+    // left | right | send_left | send_right (rows x K) | 4 + 4 K x K corners.
+    const size_t need2 = 4 * (size_t)cols + 8 * (size_t)rows + 8;
+    const size_t needk = K ? 2 * (size_t)K * cols + 4 * (size_t)rows * K + 8 * (size_t)K * K : 0;
+    SMI_TRY(ensure_halo(c, need2 + needk));
     Halo2Buf hb;
     hb.top2 = c->halo;
     hb.bot2 = hb.top2 + 2 * (size_t)cols;
@@ -206,6 +288,22 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     hb.send_right2 = hb.send_left2 + 2 * (size_t)rows;
     hb.send_corner = hb.send_right2 + 2 * (size_t)rows;
     const Halo2 h2 = hb.view();
+    HaloKBuf hk{};
+    if (K) {
+        float *p = c->halo + need2;
+        hk.top = p;
+        hk.bot = hk.top + (size_t)K * cols;
+        hk.left = hk.bot + (size_t)K * cols;
+        hk.right = hk.left + (size_t)rows * K;
+        hk.send_left = hk.right + (size_t)rows * K;
+        hk.send_right = hk.send_left + (size_t)rows * K;
+        float *q = hk.send_right + (size_t)rows * K;
+        for (int k = 0; k < 4; ++k) {
+            hk.corner[k] = q + (size_t)k * K * K;
+            hk.send_corner[k] = q + (size_t)(4 + k) * K * K;
+        }
+    }
+    const HaloK hkv = hk.view();
     // depth-1 views: row -1, row X, col -1, col Y; packed depth-1 sends
     a.halo[0] = hb.top2 + cols;
     a.halo[1] = hb.bot2;
@@ -220,97 +318,103 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
                          const_cast<float *>(a.halo[2]), const_cast<float *>(a.halo[3]), s_left, s_right, st);
     };
     auto xchg2 = [&](const float *tile, hipStream_t st) { return exchange2(c, nb, tile, rows, cols, hb, st); };
+    auto xchgk = [&](const float *tile, hipStream_t st) { return exchangek(c, nb, tile, rows, cols, K, hk, st); };
+    RingKArgs rk{};
+    rk.rows = rows;
+    rk.cols = cols;
+    rk.k = K;
+    for (int k = 0; k < 4; ++k) rk.has[k] = side_nb[k] >= 0;
+    const int diag_nb[4] = {nb.tl, nb.tr, nb.bl, nb.br};
+    for (int k = 0; k < 4; ++k) rk.has_diag[k] = diag_nb[k] >= 0;
+    rk.h = hkv;
 
     hipEvent_t ev_edge, ev_int;
     SMI_TRY(comm_event(c, 0, &ev_edge));
     SMI_TRY(comm_event(c, 1, &ev_int));
 
-    // Schedule (two streams, no host synchronisation between steps):
-    //   comm stream : [wait interior(t-1)] edge/ring(t) -> rec E_edge(t) -> exchange(t)
+    // Schedule (two streams, no host synchronisation between passes):
+    //   comm stream : [wait interior(t-1)] ring(t) -> rec E_edge(t) -> exchange(t)
     //   main stream : [wait E_edge(t-1)] interior(t)    -> rec E_int(t)
-    // The edge/ring kernel reads in(t) (interior cells from interior(t-1),
+    // The ring kernel reads in(t) (interior cells from interior(t-1),
     // halo-facing cells from its own predecessor) and the halos of
     // exchange(t-1); the interior reads only in(t), never a halo vector, so
     // neither the halo-facing cells nor the xGMI exchange sit on its path.
-    SMI_HIP_CHECK(hipEventRecord(ev_int, s));
-    SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
-    // initial halos = the neighbours' initial edges (the reference's
-    // artificial timestep t=0, stencil_smi.cl:26-29,183-224)
-    if (fused) {
-        SMI_TRY(launch_pack2(buf0, rows, cols, h2, cs));
-        SMI_TRY(xchg2(buf0, cs));
-    } else {
-        SMI_TRY(launch_pack_cols(buf0, rows, cols, a.send_left, a.send_right, cs));
-        SMI_TRY(xchg1(buf0, cs));
-    }
-
+    // Each phase (K-step passes, pairs, singles) starts from halos of the
+    // current state: the neighbours' current edges (for the first phase the
+    // reference's artificial timestep t=0, stencil_smi.cl:26-29,183-224).
     const bool overlap = g_tune.overlap != 0;
-    // ---- pairs of steps (depth-2 halos)
-    for (int p = 0; p < pairs; ++p, cur ^= 1) {
-        a2.in = bufp(cur);
-        a2.out = bufp(cur ^ 1);
-        const bool need_xchg = p < pairs - 1 || singles > 0;
+    auto phase_start = [&]() -> int {
+        SMI_HIP_CHECK(hipEventRecord(ev_int, s));
+        SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
+        return SMI_SUCCESS;
+    };
+    // one pass of a phase: ring (comm stream) + interior (main stream)
+    auto pass = [&](auto ring, auto interior, auto xchg, bool need_xchg, const float *out) -> int {
         if (overlap) {
-            SMI_TRY(launch_ring2(a2, h2, cs));
+            SMI_TRY(ring(cs));
             SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-            if (need_xchg) SMI_TRY(xchg2(a2.out, cs));
-            SMI_TRY(launch_sweep2(a2, s));
+            if (need_xchg) SMI_TRY(xchg(out, cs));
+            SMI_TRY(interior(s));
             SMI_HIP_CHECK(hipEventRecord(ev_int, s));
             SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
             SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
         } else {
             SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
             SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-            SMI_TRY(launch_ring2(a2, h2, s));
-            SMI_TRY(launch_sweep2(a2, s));
+            SMI_TRY(ring(s));
+            SMI_TRY(interior(s));
             SMI_HIP_CHECK(hipEventRecord(ev_int, s));
             SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
-            if (need_xchg) SMI_TRY(xchg2(a2.out, cs));
+            if (need_xchg) SMI_TRY(xchg(out, cs));
+        }
+        return SMI_SUCCESS;
+    };
+
+    // ---- K steps per pass (depth-K halos)
+    if (kpasses > 0) {
+        SMI_TRY(phase_start());
+        SMI_TRY(launch_packk(bufp(cur), rows, cols, K, hkv, cs));
+        SMI_TRY(xchgk(bufp(cur), cs));
+        for (int p = 0; p < kpasses; ++p, cur ^= 1) {
+            rk.in = ak.in = bufp(cur);
+            rk.out = ak.out = bufp(cur ^ 1);
+            SMI_TRY(pass([&](hipStream_t st) { return launch_ringk(rk, st); },
+                         [&](hipStream_t st) { return launch_sweepk(K, ak, st); }, xchgk, p < kpasses - 1,
+                         ak.out));
         }
     }
-    if (pairs > 0 && singles > 0) {
-        // the remaining single step reads depth-1 views of the last exchange
-        SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-        SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-        a.in = bufp(cur);
-        a.out = bufp(cur ^ 1);
-        a.send_left = a.send_right = nullptr;
-        SMI_TRY(launch_sweep(a, s));
-        cur ^= 1;
-        return SMI_SUCCESS;
+    // ---- pairs of steps (depth-2 halos)
+    if (pairs > 0) {
+        SMI_TRY(phase_start());
+        SMI_TRY(launch_pack2(bufp(cur), rows, cols, h2, cs));
+        SMI_TRY(xchg2(bufp(cur), cs));
+        for (int p = 0; p < pairs; ++p, cur ^= 1) {
+            a2.in = bufp(cur);
+            a2.out = bufp(cur ^ 1);
+            SMI_TRY(pass([&](hipStream_t st) { return launch_ring2(a2, h2, st); },
+                         [&](hipStream_t st) { return launch_sweep2(a2, st); }, xchg2, p < pairs - 1, a2.out));
+        }
     }
-
     // ---- single steps (depth-1 halos)
-    SweepArgs inner = a;  // interior launch: halo-facing sides left to the edge kernel
-    for (int k = 0; k < 4; ++k)
-        if (inner.mode[k] == SMI_SIDE_HALO) inner.mode[k] = SMI_SIDE_SKIP;
-    inner.send_left = inner.send_right = nullptr;
-    if (!overlap) {  // the full sweep reads the halos on the main stream
-        SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-        SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-    }
-    for (int t = 0; t < singles; ++t, cur ^= 1) {
-        const float *in = bufp(cur);
-        float *out = bufp(cur ^ 1);
-        const bool last = t == singles - 1;
-        a.in = inner.in = in;
-        a.out = inner.out = out;
-        if (overlap) {
-            SMI_TRY(launch_edge(a, side_mask, cs));
-            SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-            if (!last) SMI_TRY(xchg1(out, cs));
-            SMI_TRY(launch_sweep(inner, s));
-            SMI_HIP_CHECK(hipEventRecord(ev_int, s));
-            SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-            SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
-        } else {
-            SMI_TRY(launch_sweep(a, s));
-            SMI_HIP_CHECK(hipEventRecord(ev_int, s));
-            if (!last) {
-                SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
-                SMI_TRY(xchg1(out, cs));
-                SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-                SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
+    if (singles > 0) {
+        SMI_TRY(phase_start());
+        SMI_TRY(launch_pack_cols(bufp(cur), rows, cols, a.send_left, a.send_right, cs));
+        SMI_TRY(xchg1(bufp(cur), cs));
+        SweepArgs inner = a;  // interior launch: halo-facing sides left to the edge kernel
+        for (int k = 0; k < 4; ++k)
+            if (inner.mode[k] == SMI_SIDE_HALO) inner.mode[k] = SMI_SIDE_SKIP;
+        inner.send_left = inner.send_right = nullptr;
+        for (int t = 0; t < singles; ++t, cur ^= 1) {
+            a.in = inner.in = bufp(cur);
+            a.out = inner.out = bufp(cur ^ 1);
+            if (overlap) {
+                SMI_TRY(pass([&](hipStream_t st) { return launch_edge(a, side_mask, st); },
+                             [&](hipStream_t st) { return launch_sweep(inner, st); }, xchg1, t < singles - 1,
+                             a.out));
+            } else {
+                // the full sweep reads the halos itself
+                SMI_TRY(pass([&](hipStream_t) { return (int)SMI_SUCCESS; },
+                             [&](hipStream_t st) { return launch_sweep(a, st); }, xchg1, t < singles - 1, a.out));
             }
         }
     }

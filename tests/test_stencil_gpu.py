@@ -196,13 +196,16 @@ def test_full_size_8192_sweep(gpu, oracle_mod):
 
 
 # ------------------------------------------------ two steps per pass (fused) --
-def _run_fused(grid, T, PX=1, PY=1, overlap=1, ht2=0, u2=0):
+def _run_fused(grid, T, PX=1, PY=1, overlap=1, ht2=0, u2=0, k=2):
     from smi_amd import stencil
     old = stencil.get_fusion()
-    stencil.set_fusion(2, ht2, u2)
+    stencil.set_fusion(k)
+    oldk = stencil.get_fusion()
+    stencil.set_fusion(k, ht2, u2)
     try:
         return _decomposed_run(grid, T, PX, PY, overlap)
     finally:
+        stencil.set_fusion(k, oldk["rows_per_wave"], oldk["rows_in_flight"])
         stencil.set_fusion(old["steps_per_pass"], old["rows_per_wave"], old["rows_in_flight"])
 
 
@@ -246,3 +249,61 @@ def test_fused_full_size_8192(gpu, oracle_mod):
     g = oracle_mod.init_uniform(8192, 8192, seed=43)
     got = _run_fused(g, 4)
     assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 4)))
+
+
+# --------------------------------------------- K = 4, 8 steps per pass (deep) --
+@pytest.mark.parametrize("k", [4, 8])
+@pytest.mark.parametrize("shape", [(1, 4), (2, 8), (5, 8), (9, 12), (17, 260), (64, 64), (129, 500),
+                                   (300, 1028), (1000, 516)])
+def test_deep_single_tile(gpu, oracle_mod, k, shape):
+    X, Y = shape
+    g = oracle_mod.init_uniform(X, Y, seed=X + 5 * Y + k)
+    for T in (1, k - 1, k, k + 3, 2 * k + 1):
+        got = _run_fused(g, T, k=k)
+        assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, shape, T)
+
+
+@pytest.mark.parametrize("k", [4, 8])
+@pytest.mark.parametrize("ht,u", [(1, 2), (5, 4), (16, 8), (32, 2), (100, 8)])
+def test_deep_tuning_is_bit_neutral(gpu, oracle_mod, k, ht, u):
+    g = oracle_mod.init_uniform(517, 1540, seed=11)
+    got = _run_fused(g, 2 * k, ht2=ht, u2=u, k=k)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 2 * k)))
+
+
+def test_deep_config1_and_edges(gpu, oracle_mod):
+    g = oracle_mod.init_edges(256, 256)
+    assert np.array_equal(bits(_run_fused(g, 32, k=4)), bits(oracle_mod.stencil(g, 32)))
+    assert np.array_equal(bits(_run_fused(g, 32, k=8)), bits(oracle_mod.stencil(g, 32)))
+
+
+def test_deep_full_size_8192(gpu, oracle_mod):
+    g = oracle_mod.init_uniform(8192, 8192, seed=44)
+    got = _run_fused(g, 8, k=4)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 8)))
+
+
+@pytest.mark.parametrize("overlap", [0, 1])
+@pytest.mark.parametrize("k", [4, 8])
+@pytest.mark.parametrize("pxpy", [(2, 1), (1, 2), (2, 2), (2, 4), (3, 3)])
+def test_deep_decomposed(gpu, oracle_mod, k, pxpy, overlap):
+    """K-step passes with depth-K halos and K x K corner blocks, then the
+    pair and single-step phases for the remainder (T = 2K+3)."""
+    PX, PY = pxpy
+    g = oracle_mod.init_uniform(72 * PX, 136 * PY, seed=PX * 11 + PY + k)
+    for T in (k, 2 * k + 3):
+        got = _run_fused(g, T, PX, PY, overlap, k=k)
+        assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, pxpy, T)
+
+
+@pytest.mark.parametrize("k", [4, 8])
+def test_deep_decomposed_small_tiles(gpu, oracle_mod, k):
+    # exactly 2K x 2K tiles (smallest deep tile), ring blocks larger than tiles
+    g = oracle_mod.init_uniform(4 * k, 6 * k, seed=k)
+    assert np.array_equal(bits(_run_fused(g, 3 * k + 1, 2, 3, k=k)), bits(oracle_mod.stencil(g, 3 * k + 1)))
+    # tiles below 2K fall back to pairs/singles
+    g = oracle_mod.init_uniform(2 * k - 4, 4 * k, seed=k + 1)
+    assert np.array_equal(bits(_run_fused(g, 2 * k, 2, 2, k=k)), bits(oracle_mod.stencil(g, 2 * k)))
+    # config 1 (256^2, 2x2, 32 steps) through the deep path
+    g = oracle_mod.init_edges(256, 256)
+    assert np.array_equal(bits(_run_fused(g, 32, 2, 2, k=k)), bits(oracle_mod.stencil_decomposed(g, 32, 2, 2)))
