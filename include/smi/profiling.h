@@ -19,7 +19,8 @@ typedef enum {
     SMI_PROF_STENCIL_EDGE = 1,   /* halo-edge kernel (multi-rank overlap)  */
     SMI_PROF_REDUCE_FOLD = 2,
     SMI_PROF_GEMV = 3,
-    SMI_PROF_NUM = 4
+    SMI_PROF_STENCIL_SWEEPK = 4, /* the K-step (temporally blocked) sweep  */
+    SMI_PROF_NUM = 5
 } SMI_ProfKernel;
 
 int smi_prof_enable(int enable);

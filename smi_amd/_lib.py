@@ -29,7 +29,7 @@ SMI_ADD, SMI_MAX, SMI_MIN = 0, 1, 2
 # include/smi/stencil.h
 SIDE_COPY, SIDE_HALO, SIDE_SKIP = 0, 1, 2
 # include/smi/profiling.h
-PROF_STENCIL_SWEEP, PROF_STENCIL_EDGE, PROF_REDUCE_FOLD, PROF_GEMV = 0, 1, 2, 3
+PROF_STENCIL_SWEEP, PROF_STENCIL_EDGE, PROF_REDUCE_FOLD, PROF_GEMV, PROF_STENCIL_SWEEPK = 0, 1, 2, 3, 4
 
 
 class SMIError(RuntimeError):

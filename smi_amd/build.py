@@ -28,6 +28,10 @@ CXXFLAGS = [
     f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
     f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
 ]
+# Per-file extras.  stencilk.hip spells out which adds are packed
+# (v_pk_add_f32 on aligned pairs); the SLP vectorizer would pack the
+# shuffled (S+W)/(+E) adds too and pay a register move for each pair.
+FILE_FLAGS = {"stencilk.hip": ["-fno-slp-vectorize"]}
 LDFLAGS = ["-shared", f"-L{ROCM}/lib", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"]
 
 
@@ -64,7 +68,7 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     procs = []
     for src in sources():
         obj = os.path.join(out_dir, os.path.basename(src) + ".o")
-        cmd = [hipcc, *flags, "-c", src, "-o", obj]
+        cmd = [hipcc, *flags, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

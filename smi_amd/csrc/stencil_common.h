@@ -65,11 +65,11 @@ struct Tuning {
     int u = 16;         // rows in flight per batch
     int nt = 1;         // non-temporal stores
     int overlap = 1;    // overlap halo exchange with the interior sweep
-    int fuse = 2;       // Jacobi steps per pass over HBM (1 or 2)
+    int fuse = 12;      // Jacobi steps per pass over HBM (1, 2, 4, 8 or 12)
     int ht2 = 8;        // rows per wave (two-step sweep)
     int u2 = 8;         // rows in flight per batch (two-step sweep)
-    int htk = 32;       // rows per wave (K-step sweep, K >= 4)
-    int uk = 8;         // rows in flight per batch (K-step sweep)
+    int htk = 0;        // rows per wave (K-step sweep, K >= 4); 0 = one round of resident waves
+    int uk = 3;         // rows per load batch (K-step sweep: fixed at 3, the slot ring period)
 };
 extern Tuning g_tune;
 

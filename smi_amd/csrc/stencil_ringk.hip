@@ -1,4 +1,4 @@
-// stencil_ringk.hip -- the halo-facing ring of a K-step pass (K = 4, 8).
+// stencil_ringk.hip -- the halo-facing ring of a K-step pass (K = 4, 8, 12).
 //
 // In a multi-rank run with K Jacobi steps per pass, every tile cell within K
 // of a side that has a neighbour depends on that neighbour's cells (up to K
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void packk_kernel(const float *in, int X, int 
 
 int launch_ringk(RingKArgs a, hipStream_t s) {
     const int X = a.rows, Y = a.cols, K = a.k;
-    SMI_ARG_CHECK(K == 4 || K == 8, "ring: K must be 4 or 8");
+    SMI_ARG_CHECK(K == 4 || K == 8 || K == 12, "ring: K must be 4, 8 or 12");
     SMI_ARG_CHECK(X >= 2 * K && Y >= 2 * K, "ring: tile smaller than 2K");
     // bands: top rows [0,K), bottom rows [X-K,X) (full width); left/right
     // columns over the rows the top/bottom bands leave
@@ -142,10 +142,11 @@ int launch_ringk(RingKArgs a, hipStream_t s) {
     if (nb == 0) return SMI_SUCCESS;
     int tok = -1;
     if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_EDGE, s, &tok));
-    if (K == 4)
-        hipLaunchKernelGGL(ringk_kernel<4>, dim3(nb), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(ringk_kernel<8>, dim3(nb), dim3(256), 0, s, a);
+    switch (K) {
+    case 4: hipLaunchKernelGGL(ringk_kernel<4>, dim3(nb), dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(ringk_kernel<8>, dim3(nb), dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(ringk_kernel<12>, dim3(nb), dim3(256), 0, s, a); break;
+    }
     SMI_HIP_CHECK(hipGetLastError());
     if (tok >= 0) SMI_TRY(prof_end(tok, s));
     return SMI_SUCCESS;

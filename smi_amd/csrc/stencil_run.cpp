@@ -161,18 +161,22 @@ extern "C" {
 
 int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_flight) {
     if (steps_per_pass > 0) {
-        SMI_ARG_CHECK(steps_per_pass == 1 || steps_per_pass == 2 || steps_per_pass == 4 || steps_per_pass == 8,
-                      "steps_per_pass must be 1, 2, 4 or 8");
+        SMI_ARG_CHECK(steps_per_pass == 1 || steps_per_pass == 2 || steps_per_pass == 4 || steps_per_pass == 8 ||
+                          steps_per_pass == 12,
+                      "steps_per_pass must be 1, 2, 4, 8 or 12");
         g_tune.fuse = steps_per_pass;
     }
     // rows_per_wave / rows_in_flight tune the kernel of the current setting
     const bool deep = g_tune.fuse >= 4;
     if (rows_per_wave > 0) (deep ? g_tune.htk : g_tune.ht2) = rows_per_wave;
-    if (rows_in_flight > 0) {
+    if (rows_per_wave < 0 && deep) g_tune.htk = 0;  // automatic: one round of resident waves
+    if (rows_in_flight > 0 && !deep) {
         SMI_ARG_CHECK(rows_in_flight == 1 || rows_in_flight == 2 || rows_in_flight == 4 || rows_in_flight == 8,
                       "rows_in_flight must be 1, 2, 4 or 8");
-        (deep ? g_tune.uk : g_tune.u2) = rows_in_flight;
+        g_tune.u2 = rows_in_flight;
     }
+    // the K-step sweep loads in batches of 3 rows (its slot-ring period);
+    // rows_in_flight is accepted and ignored there
     return SMI_SUCCESS;
 }
 

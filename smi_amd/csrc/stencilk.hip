@@ -3,29 +3,185 @@
 // Same per-cell arithmetic as every other stencil kernel here
 // (stencil_smi.cl:153-156, global-edge cells copied per :143-151), applied K
 // times inside one streaming pass.  Each wave owns a 256-column window of the
-// input and walks it down the rows; every incoming input row advances a
-// pipeline of K levels (level l lags l rows behind the input, each keeping a
-// two-row window in registers), and only level K is stored.  The window is
-// 256 input columns wide but outputs only the central 256-2K: each level
-// loses one valid column on each side, so adjacent windows overlap by 2K
-// columns instead of fetching strip-edge extras (no cross-lane broadcasts,
-// 1.6 % redundant columns at K=4).  HBM traffic per pass is that of a single
-// step, so the algorithmic 8 B/cell/step are moved up to K times faster.
+// input and walks it down a block of rows; every incoming input row advances
+// a pipeline of K levels (level l lags l rows behind the input) and only
+// level K is stored.  The window is 256 input columns wide but stores only
+// the central 256-2K: each level loses one valid column per side, so
+// adjacent windows overlap by 2K columns instead of fetching strip-edge
+// extras (no cross-lane broadcasts).  HBM traffic per pass is that of a
+// single step, so the algorithmic 8 B/cell/step move up to K times faster.
+//
+// Register pipeline.  Level l keeps its last three rows in a 3-slot ring,
+// slot = (input row index) mod 3; the loop body covers 6 input rows (two
+// batches of 3, each batch's loads issued one batch ahead), so every slot
+// index is a compile-time constant and no value is ever moved between
+// registers.  The first 2K input rows of a row block only prime the
+// pipeline; that prologue is unrolled with compile-time row indices and
+// evaluates level l only from input row 2l on (the rows it must produce).
+// Waves whose rows or columns touch a global edge run a variant with the
+// copy rules; all others run without any per-cell selects.
 //
 // The kernel computes an arbitrary output rectangle [row_lo,row_hi) x
-// [col_lo,col_hi) of the tile from input rows/columns within K of it, so the
-// same kernel is the single-tile sweep (whole tile) and, in multi-rank runs,
-// the interior sweep that stays K cells clear of every halo-facing side.
+// [col_lo,col_hi) of the tile from input cells within K of it, so it is the
+// single-tile sweep (whole tile) and, in multi-rank runs, the interior sweep
+// that stays K cells clear of every halo-facing side.
+#include <type_traits>
+
 #include "stencil_common.h"
 
 namespace smi {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// lane i <- lane i-1 / i+1 (DPP wave_shr:1 / wave_shl:1).  Lanes 0 / 63 get
+// whatever the hardware leaves (they only ever feed non-stored columns), so
+// the destination needs no initialisation.
+__device__ __forceinline__ float shr1_any(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float shl1_any(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
+}
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_from(F &f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for_from<I + 1, N>(f);
+    }
+}
+// f(integral_constant<0>) ... f(integral_constant<N-1>), fully unrolled
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_from<0, N>(f);
+}
+
+template <int K, int U, bool NT>
+struct SweepK {
+    static_assert(K % 4 == 0 && K >= 4 && K <= 12, "K must be a multiple of 4 (float4 lanes)");
+    static_assert(U % 3 == 0, "batch must be a multiple of the 3-slot ring");
+    static constexpr int LL = K / 4;  // lanes per side that never store
+    static constexpr int PRO = 2 * K; // prologue input rows
+
+    const float *__restrict__ in;
+    float *__restrict__ out;
+    int rows, cols;
+    int o0, o1;       // output rows of this wave
+    int r_begin;      // first input row (o0 - K)
+    int cl, cb;       // clamped load column / first column of this lane
+    int voff;         // store byte offset in the row (out of range: no store)
+    int row_bytes;
+    bool st, copyL, copyR, gT, gB;
+    float4 W[K][3];   // level 0..K-1, slot = input row index mod 3
+
+    __device__ __forceinline__ float4 ld(int t) const {
+        const int r = min(max(r_begin + t, 0), rows - 1);
+        return *reinterpret_cast<const float4 *>(in + (size_t)r * cols + cl);
+    }
+
+    template <bool EDGE>
+    __device__ __forceinline__ float4 step(int i, const float4 &n, const float4 &c, const float4 &s) const {
+        const float w = shr1_any(c.w);
+        const float e = shl1_any(c.x);
+        // ((S + W) + E) element-wise, then (+ N) and (x 0.25) on packed
+        // pairs (v_pk_add_f32 / v_pk_mul_f32: same IEEE single-precision
+        // round-to-nearest results as the scalar ops, never contracted)
+        f32x2 sw01 = {__fadd_rn(s.x, w), __fadd_rn(s.y, c.x)};
+        f32x2 sw23 = {__fadd_rn(s.z, c.y), __fadd_rn(s.w, c.z)};
+        f32x2 swe01 = {__fadd_rn(sw01.x, c.y), __fadd_rn(sw01.y, c.z)};
+        f32x2 swe23 = {__fadd_rn(sw23.x, c.w), __fadd_rn(sw23.y, e)};
+        const f32x2 q = {0.25f, 0.25f};
+        const f32x2 o01 = (swe01 + f32x2{n.x, n.y}) * q;
+        const f32x2 o23 = (swe23 + f32x2{n.z, n.w}) * q;
+        float4 o;
+        o.x = o01.x;
+        o.y = o01.y;
+        o.z = o23.x;
+        o.w = o23.y;
+        if constexpr (EDGE) {
+            const bool rcopy = (i == 0 && gT) || (i == rows - 1 && gB);
+            o.x = (rcopy || copyL) ? c.x : o.x;
+            o.y = rcopy ? c.y : o.y;
+            o.z = rcopy ? c.z : o.z;
+            o.w = (rcopy || copyR) ? c.w : o.w;
+        }
+        return o;
+    }
+
+    // Input row t (index from r_begin) arrives with value x; PH = t mod 3.
+    template <bool EDGE, int PH>
+    __device__ __forceinline__ void advance(int t, const float4 &x) {
+        W[0][PH] = x;
+        float4 v;
+        static_for<K>([&](auto L) {
+            constexpr int l = L + 1;
+            // level l-1 rows produced at inputs t-2, t-1, t live in slots PH+1, PH+2, PH (mod 3)
+            v = step<EDGE>(r_begin + t - l, W[l - 1][(PH + 1) % 3], W[l - 1][(PH + 2) % 3], W[l - 1][PH]);
+            if constexpr (l < K) W[l][PH] = v;
+        });
+        const int j = o0 + (t - PRO);  // level-K row produced by input t
+        store_row(j, v);
+    }
+
+    // Branch-free predicated store: a buffer store through a per-row
+    // descriptor whose record count is the row's bytes (0 for rows past o1);
+    // lanes that must not store carry an offset beyond it and the hardware
+    // range check drops them.  No branch splits the unrolled rows, so the
+    // scheduler interleaves their dependency chains.
+    __device__ __forceinline__ void store_row(int j, const float4 &v) const {
+        const int jj = __builtin_amdgcn_readfirstlane(min(j, rows - 1));
+        const int nrec = __builtin_amdgcn_readfirstlane(j < o1 ? row_bytes : 0);
+        __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(out + (size_t)jj * cols, (short)0, nrec, 0x00020000);
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 d = {__builtin_bit_cast(unsigned int, v.x), __builtin_bit_cast(unsigned int, v.y),
+                         __builtin_bit_cast(unsigned int, v.z), __builtin_bit_cast(unsigned int, v.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(d, rs, voff, 0, NT ? 2 : 0);
+    }
+
+    template <bool EDGE>
+    __device__ __forceinline__ void run() {
+        // prologue: input rows 0 .. 2K-1, compile-time indices
+        static_for<PRO>([&](auto T) {
+            constexpr int t = T;
+            const float4 x = ld(t);
+            W[0][t % 3] = x;
+            static_for<K>([&](auto L) {
+                constexpr int l = L + 1;
+                if constexpr (t >= 2 * l) {
+                    const float4 v = step<EDGE>(r_begin + t - l, W[l - 1][(t + 1) % 3], W[l - 1][(t + 2) % 3],
+                                                W[l - 1][t % 3]);
+                    if constexpr (l < K) W[l][t % 3] = v;
+                }
+            });
+        });
+        // steady state: 2U input rows per iteration, loads one batch ahead
+        const int n_in = (o1 - o0) + PRO;
+        float4 A[U], B[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) A[u] = ld(PRO + u);
+        for (int t = PRO; t < n_in; t += 2 * U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) B[u] = ld(t + U + u);
+            static_for<U>([&](auto V) {
+                constexpr int ph = (PRO + V) % 3;
+                advance<EDGE, ph>(t + V, A[V]);
+            });
+            if (t + U >= n_in) break;  // uniform
+#pragma unroll
+            for (int u = 0; u < U; ++u) A[u] = ld(t + 2 * U + u);
+            static_for<U>([&](auto V) {
+                constexpr int ph = (PRO + U + V) % 3;
+                advance<EDGE, ph>(t + U + V, B[V]);
+            });
+        }
+    }
+};
+
 template <int K, int U, bool NT>
 __global__ __launch_bounds__(256) void sweepk_kernel(const float *__restrict__ in, float *__restrict__ out,
                                                      SweepKArgs a, int nstrips, int nrb, int ht) {
-    static_assert(K % 4 == 0 && K >= 4 && K <= 16, "K must be a multiple of 4 (float4 lanes)");
     constexpr int SW = 256 - 2 * K;  // output columns per window
-    constexpr int LL = K / 4;        // lanes on each side that never store
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
     const int task = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
@@ -33,80 +189,31 @@ __global__ __launch_bounds__(256) void sweepk_kernel(const float *__restrict__ i
     const int strip = task - rb * nstrips;
     if (rb >= nrb) return;  // wave-uniform
 
-    const int rows = a.rows, cols = a.cols;
-    const int o0 = a.row_lo + rb * ht;
-    const int o1 = min(o0 + ht, a.row_hi);
+    SweepK<K, U, NT> w;
+    w.in = in;
+    w.out = out;
+    w.rows = a.rows;
+    w.cols = a.cols;
+    w.o0 = a.row_lo + rb * ht;
+    w.o1 = min(w.o0 + ht, a.row_hi);
+    w.r_begin = w.o0 - K;
     const int cs = a.col_lo + strip * SW;
-    const int cb = cs - K + 4 * lane;                 // this lane's first column
-    const int cl = min(max(cb, 0), cols - 4);         // clamped load column
-    const bool st = lane >= LL && lane < 64 - LL && cb < a.col_hi;
-    const bool copyL = a.gL && cb == 0;
-    const bool copyR = a.gR && cb + 4 == cols;
-    const bool gT = a.gT, gB = a.gB;
-
-    auto ld = [&](int r) -> float4 {
-        const size_t i = (size_t)min(max(r, 0), rows - 1) * cols + cl;
-        return *reinterpret_cast<const float4 *>(in + i);
-    };
-    // level value at row i from (N, C, S) of the level below
-    auto step = [&](int i, const float4 &n, const float4 &c, const float4 &s) -> float4 {
-        const bool rcopy = (i == 0 && gT) || (i == rows - 1 && gB);
-        const float w = wave_shr1(c.w);
-        const float e = wave_shl1(c.x);
-        float4 o;
-        o.x = jacobi(s.x, w, c.y, n.x);
-        o.y = jacobi(s.y, c.x, c.z, n.y);
-        o.z = jacobi(s.z, c.y, c.w, n.z);
-        o.w = jacobi(s.w, c.z, e, n.w);
-        o.x = (rcopy || copyL) ? c.x : o.x;
-        o.y = rcopy ? c.y : o.y;
-        o.z = rcopy ? c.z : o.z;
-        o.w = (rcopy || copyR) ? c.w : o.w;
-        return o;
-    };
-
-    // P[l][0], P[l][1]: level-l rows (r-l-2, r-l-1) when input row r arrives
-    float4 P[K][2];
-#pragma unroll
-    for (int l = 0; l < K; ++l) P[l][0] = P[l][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-
-    // Push input row r through the K levels.  The first 2K rows only prime
-    // the pipeline (their level-K rows lie above o0 and are not stored).
-    auto advance = [&](int r, const float4 &x) {
-        float4 s = x;
-#pragma unroll
-        for (int l = 1; l <= K; ++l) {
-            const float4 v = step(r - l, P[l - 1][0], P[l - 1][1], s);
-            P[l - 1][0] = P[l - 1][1];
-            P[l - 1][1] = s;
-            s = v;
-        }
-        const int j = r - K;
-        if (j >= o0 && st) {
-            float *op = out + (size_t)j * cols + cb;
-            store4<NT>(op, s);
-        }
-    };
-
-    const int r_begin = o0 - K, r_end = o1 + K;  // input rows [r_begin, r_end)
-    float4 A[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) A[u] = ld(min(r_begin + u, r_end - 1));
-    for (int r = r_begin; r < r_end; r += U) {
-        float4 B[U];
-        const bool more = r + U < r_end;  // uniform
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) B[u] = ld(min(r + U + u, r_end - 1));
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (r + u < r_end) advance(r + u, A[u]);
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) A[u] = B[u];
-        }
-    }
+    w.cb = cs - K + 4 * lane;
+    w.cl = min(max(w.cb, 0), a.cols - 4);
+    w.st = lane >= SweepK<K, U, NT>::LL && lane < 64 - SweepK<K, U, NT>::LL && w.cb < a.col_hi;
+    w.row_bytes = a.cols * 4;
+    w.voff = w.st ? w.cb * 4 : 0x7ffffff0;
+    w.copyL = a.gL && w.cb == 0;
+    w.copyR = a.gR && w.cb + 4 == a.cols;
+    w.gT = a.gT;
+    w.gB = a.gB;
+    // rows any level touches: [o0 - 2K, o1 + K + 5); columns: [cs - K, cs - K + 256)
+    const bool edge = (a.gT && w.o0 - 2 * K <= 0) || (a.gB && w.o1 + K + 6 >= a.rows) ||
+                      (a.gL && cs - K <= 0) || (a.gR && cs - K + 256 >= a.cols);
+    if (edge)
+        w.template run<true>();
+    else
+        w.template run<false>();
 }
 
 template <int K, int U>
@@ -119,34 +226,52 @@ static void launch_k(const SweepKArgs &a, int nstrips, int nrb, int ht, int bloc
                            nrb, ht);
 }
 
-template <int K>
-static int launch_k_u(const SweepKArgs &a, int nstrips, int nrb, int ht, int blocks, int u, bool nt,
-                      hipStream_t s) {
-    switch (u) {
-    case 2: launch_k<K, 2>(a, nstrips, nrb, ht, blocks, nt, s); break;
-    case 4: launch_k<K, 4>(a, nstrips, nrb, ht, blocks, nt, s); break;
-    default: launch_k<K, 8>(a, nstrips, nrb, ht, blocks, nt, s); break;
-    }
-    return SMI_SUCCESS;
+// resident waves of sweepk<K> on this device (one round of the grid)
+template <int K, int U>
+static int resident_waves() {
+    static int cached[64] = {};  // per device
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (cached[dev]) return cached[dev];
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweepk_kernel<K, U, true>, 256, 0) != hipSuccess)
+        return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cached[dev] = per_cu * cus * 4;
+    return cached[dev];
 }
 
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
     if (a.row_hi <= a.row_lo || a.col_hi <= a.col_lo) return SMI_SUCCESS;
+    SMI_ARG_CHECK(K == 4 || K == 8 || K == 12, "sweepk: steps per pass must be 4, 8 or 12");
     SMI_ARG_CHECK(a.cols % 4 == 0 && a.col_lo % 4 == 0 && a.col_hi % 4 == 0, "sweepk: columns not float4 aligned");
     SMI_ARG_CHECK(a.row_lo >= 0 && a.row_hi <= a.rows && a.col_lo >= 0 && a.col_hi <= a.cols,
                   "sweepk: output rectangle outside the tile");
-    const int ht = std::max(1, g_tune.htk);
     const int sw = 256 - 2 * K;
     const int nstrips = (a.col_hi - a.col_lo + sw - 1) / sw;
-    const int nrb = (a.row_hi - a.row_lo + ht - 1) / ht;
+    const int out_rows = a.row_hi - a.row_lo;
+    int ht = g_tune.htk;
+    if (ht <= 0) {
+        // auto: one round of resident waves, each a tall row block of its strip
+        int waves = 0;
+        switch (K) {
+        case 4: waves = resident_waves<4, 3>(); break;
+        case 8: waves = resident_waves<8, 3>(); break;
+        default: waves = resident_waves<12, 3>(); break;
+        }
+        const int per_strip = std::max(1, waves / nstrips);
+        ht = std::max(2 * K, (out_rows + per_strip - 1) / per_strip);
+    }
+    const int nrb = (out_rows + ht - 1) / ht;
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
     int tok = -1;
-    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEP, s, &tok));
+    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok));
+    const bool nt = g_tune.nt;
     switch (K) {
-    case 4: launch_k_u<4>(a, nstrips, nrb, ht, blocks, g_tune.uk, g_tune.nt, s); break;
-    case 8: launch_k_u<8>(a, nstrips, nrb, ht, blocks, g_tune.uk, g_tune.nt, s); break;
-    default: set_error("sweepk: steps per pass must be 4 or 8"); return SMI_ERR_INVALID_ARG;
+    case 4: launch_k<4, 3>(a, nstrips, nrb, ht, blocks, nt, s); break;
+    case 8: launch_k<8, 3>(a, nstrips, nrb, ht, blocks, nt, s); break;
+    default: launch_k<12, 3>(a, nstrips, nrb, ht, blocks, nt, s); break;
     }
     SMI_HIP_CHECK(hipGetLastError());
     if (tok >= 0) SMI_TRY(prof_end(tok, s));

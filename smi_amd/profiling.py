@@ -9,6 +9,7 @@ SWEEP = _lib.PROF_STENCIL_SWEEP
 EDGE = _lib.PROF_STENCIL_EDGE
 REDUCE_FOLD = _lib.PROF_REDUCE_FOLD
 GEMV = _lib.PROF_GEMV
+SWEEPK = _lib.PROF_STENCIL_SWEEPK
 
 
 def enable(on: bool = True) -> None:

@@ -205,7 +205,7 @@ def _run_fused(grid, T, PX=1, PY=1, overlap=1, ht2=0, u2=0, k=2):
     try:
         return _decomposed_run(grid, T, PX, PY, overlap)
     finally:
-        stencil.set_fusion(k, oldk["rows_per_wave"], oldk["rows_in_flight"])
+        stencil.set_fusion(k, oldk["rows_per_wave"] or -1, oldk["rows_in_flight"])
         stencil.set_fusion(old["steps_per_pass"], old["rows_per_wave"], old["rows_in_flight"])
 
 
@@ -252,7 +252,7 @@ def test_fused_full_size_8192(gpu, oracle_mod):
 
 
 # --------------------------------------------- K = 4, 8 steps per pass (deep) --
-@pytest.mark.parametrize("k", [4, 8])
+@pytest.mark.parametrize("k", [4, 8, 12])
 @pytest.mark.parametrize("shape", [(1, 4), (2, 8), (5, 8), (9, 12), (17, 260), (64, 64), (129, 500),
                                    (300, 1028), (1000, 516)])
 def test_deep_single_tile(gpu, oracle_mod, k, shape):
@@ -263,7 +263,7 @@ def test_deep_single_tile(gpu, oracle_mod, k, shape):
         assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, shape, T)
 
 
-@pytest.mark.parametrize("k", [4, 8])
+@pytest.mark.parametrize("k", [4, 8, 12])
 @pytest.mark.parametrize("ht,u", [(1, 2), (5, 4), (16, 8), (32, 2), (100, 8)])
 def test_deep_tuning_is_bit_neutral(gpu, oracle_mod, k, ht, u):
     g = oracle_mod.init_uniform(517, 1540, seed=11)
@@ -284,7 +284,7 @@ def test_deep_full_size_8192(gpu, oracle_mod):
 
 
 @pytest.mark.parametrize("overlap", [0, 1])
-@pytest.mark.parametrize("k", [4, 8])
+@pytest.mark.parametrize("k", [4, 8, 12])
 @pytest.mark.parametrize("pxpy", [(2, 1), (1, 2), (2, 2), (2, 4), (3, 3)])
 def test_deep_decomposed(gpu, oracle_mod, k, pxpy, overlap):
     """K-step passes with depth-K halos and K x K corner blocks, then the
@@ -296,7 +296,7 @@ def test_deep_decomposed(gpu, oracle_mod, k, pxpy, overlap):
         assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, pxpy, T)
 
 
-@pytest.mark.parametrize("k", [4, 8])
+@pytest.mark.parametrize("k", [4, 8, 12])
 def test_deep_decomposed_small_tiles(gpu, oracle_mod, k):
     # exactly 2K x 2K tiles (smallest deep tile), ring blocks larger than tiles
     g = oracle_mod.init_uniform(4 * k, 6 * k, seed=k)

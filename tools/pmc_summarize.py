@@ -13,7 +13,7 @@ import csv
 import json
 import sys
 
-KERNEL = "sweep"  # matches sweep_kernel and sweep2_kernel
+KERNEL = "sweep"  # matches sweep_kernel, sweep2_kernel and sweepk_kernel
 
 
 def rows(path):
@@ -49,7 +49,7 @@ def main():
     f = sorted(fetch)[len(fetch) // 2]
     w = sorted(write)[len(write) // 2]
     d = {
-        "kernel": "sweep2_kernel" if steps_per_launch == 2 else "sweep_kernel",
+        "kernel": {1: "sweep_kernel", 2: "sweep2_kernel"}.get(steps_per_launch, f"sweepk_kernel<{steps_per_launch}>"),
         "cells": cells,
         "dispatches": [len(fetch), len(write)],
         "FETCH_SIZE_KiB_median": f,

@@ -23,8 +23,10 @@ def main():
     a = torch.rand((n, n), device="cuda")
     b = torch.empty_like(a)
     grid = {2: itertools.product([8, 16], [8]),
-            4: itertools.product([16, 32, 64, 128], [2, 4, 8]),
-            8: itertools.product([32, 64, 128], [2, 4, 8])}
+            4: itertools.product([-1, 48, 96], [4, 8]),
+            8: itertools.product([-1, 48, 96], [4, 8]),
+            12: itertools.product([-1, 48, 96], [4, 8]),
+            16: itertools.product([-1, 64, 128], [4, 8])}
     settings = [(k, ht, u) for k in ks for (ht, u) in grid[k]]
     res = {}
     for rnd in range(3):
