@@ -13,11 +13,14 @@ HBM before the timed region; the timed region is exactly K steps bracketed by
 a barrier + device synchronize on both sides; the time is the max over ranks.
 
 The JSON line also carries:
-  roofline      -- the sweep kernel: algorithmic 8 B/cell per launch divided
-                   by its average duration (HIP events around every launch,
-                   on the launch stream, inside the timed region), vs the
-                   8 TB/s HBM3E peak; `traffic` is HBM bytes per launch from
-                   the rocprofv3 PMC pass committed under profiles/ (or null)
+  roofline      -- the dominant sweep kernel (the K-step sweepk_kernel by
+                   default, K = 12 Jacobi steps per pass over HBM): algorithmic
+                   8 B/cell/step x cells x K per launch divided by its average
+                   duration (HIP events around every launch, on the launch
+                   stream, inside the timed region), vs the 8 TB/s HBM3E peak
+                   -- above 1 because of temporal blocking; `traffic` is the
+                   HBM bytes per launch from the rocprofv3 PMC passes committed
+                   under profiles/ and `hbm_frac` = traffic / launch time / peak
   cpu_baseline  -- the oracle's C restatement of the reference stencil
                    (OpenMP) timed on this host on a bounded sample (rank 0,
                    N=1 only)
@@ -53,25 +56,26 @@ def decomposition(n: int) -> tuple[int, int]:
 
 def cpu_baseline(budget_s: float = 2.0) -> dict:
     """Oracle (C restatement of the reference stencil, all host threads):
-    about budget_s of wall time (x threads = ~20-30 core-seconds)."""
+    chunks of steps until about budget_s of wall time has passed (x threads
+    = ~20-30 core-seconds)."""
     import oracle
     threads = min(16, os.cpu_count() or 1)
     g = oracle.init_uniform(TILE, TILE, seed=42)
     oracle.stencil(g, 2, threads=threads)  # warm: page faults, thread pool
-    t0 = time.perf_counter()
-    oracle.stencil(g, 4, threads=threads)
-    per_step = (time.perf_counter() - t0) / 4
-    steps = max(4, min(400, int(budget_s / max(per_step, 1e-4))))
-    t0 = time.perf_counter()
-    oracle.stencil(g, steps, threads=threads)
-    dt = time.perf_counter() - t0
+    steps, dt = 0, 0.0
+    chunk = 4
+    while dt < budget_s:
+        t0 = time.perf_counter()
+        g = oracle.stencil(g, chunk, threads=threads)
+        dt += time.perf_counter() - t0
+        steps += chunk
     return {
         "value": round(TILE * TILE * steps / dt / 1e9, 3),
         "unit": "GCell/s",
         "cores": threads,
         "kind": "port",
         "sample": f"{TILE}x{TILE} fp32 Jacobi, {steps} steps, OpenMP C restatement "
-                  f"(oracle/smi_oracle.c) of stencil_smi.cl:117-165, {dt:.1f} s wall",
+                  f"(oracle/smi_oracle.c) of stencil_smi.cl:117-165, {dt:.1f} s wall on {threads} threads",
     }
 
 

@@ -52,8 +52,8 @@ int smi_stencil_step(const float *in, float *out, int x_local, int y_local,
  * dedicated stream, overlapped with the interior sweep.  buf0 holds the
  * initial tile; buf1 is scratch of the same size.  On return *result_index
  * (0 or 1) names the buffer holding the final tile (like the reference's
- * half timesteps%2, stencil_smi.cpp:344; with two-step fusion the index is
- * (pairs + remaining single steps) % 2).  Asynchronous w.r.t. the host
+ * half timesteps%2, stencil_smi.cpp:344; with fusion the index is
+ * (K-step passes + pairs + remaining single steps) % 2).  Asynchronous w.r.t. the host
  * except for transport rendezvous. */
 int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local,
                     int y_local, int px, int py, int timesteps,
@@ -67,12 +67,18 @@ int smi_stencil_set_tuning(int rows_per_wave, int rows_in_flight,
 int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
                            int *nontemporal_stores, int *overlap);
 
-/* Temporal blocking: steps_per_pass = 2 fuses two Jacobi steps into one
- * pass over HBM (same per-cell arithmetic, bit-identical result; multi-rank
- * runs then exchange depth-2 halos -- two rows/columns per side neighbour
- * and one corner cell per diagonal neighbour -- once per pair of steps).
- * rows_per_wave / rows_in_flight tune the fused kernel (1, 2, 4 or 8).
- * Tiles smaller than 4 x 8 always run single steps.  Pass <= 0 to keep. */
+/* Temporal blocking: steps_per_pass = K in {2, 4, 8, 12} fuses K Jacobi
+ * steps into one pass over HBM (same per-cell arithmetic, bit-identical
+ * result).  Multi-rank runs then exchange depth-K halos -- K rows/columns per
+ * side neighbour and a K x K corner block per diagonal neighbour -- once per
+ * K steps; a ring kernel computes the K-wide halo-facing band while the
+ * interior sweep runs.  Default K = 12.  The bulk of a run uses K-step
+ * passes, the remainder (timesteps % K) pairs and then single steps; tiles
+ * smaller than 2K x 2K in a multi-rank run skip the K-step passes, tiles
+ * smaller than 4 x 8 run single steps only.
+ * rows_per_wave: rows per wave of the active fused kernel (K >= 4: -1 =
+ * automatic, one round of resident waves); rows_in_flight (1, 2, 4 or 8)
+ * tunes the two-step kernel and is ignored for K >= 4.  Pass 0 to keep. */
 int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_flight);
 int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in_flight);
 

@@ -23,7 +23,7 @@ def run(PX, PY, n, steps, overlap):
         with torch.cuda.stream(s):
             t = torch.rand((n, n), device="cuda")
             sc = torch.empty_like(t)
-            stencil.run(comm, t, 4, PX, PY, sc)
+            stencil.run(comm, t, 24, PX, PY, sc)
             s.synchronize()
             t0 = time.perf_counter()
             stencil.run(comm, t, steps, PX, PY, sc)
@@ -34,7 +34,7 @@ def run(PX, PY, n, steps, overlap):
     profiling.enable(True)
     t = max(grp.run(fn))
     profiling.enable(False)
-    sw = profiling.read(profiling.SWEEP)
+    sw = profiling.read(profiling.SWEEPK if stencil.get_fusion()["steps_per_pass"] >= 4 else profiling.SWEEP)
     ed = profiling.read(profiling.EDGE)
     print(json.dumps({"decomp": f"{PX}x{PY}", "overlap": overlap,
                       "sweep_avg_ms": sw[0] / max(sw[1], 1), "sweep_n": sw[1],
@@ -45,7 +45,9 @@ def run(PX, PY, n, steps, overlap):
 def main():
     smi_amd.load()
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-    steps = 50
+    steps = 120
+    if len(sys.argv) > 2:
+        stencil.set_fusion(int(sys.argv[2]))
     base = run(1, 1, n, steps, 1)
     print(json.dumps({"decomp": "1x1", "ms_per_step": base / steps * 1e3}), flush=True)
     for (PX, PY) in ((1, 2), (2, 1), (2, 2)):

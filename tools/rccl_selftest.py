@@ -64,7 +64,7 @@ def main():
         t = torch.from_numpy(tiles[rank]).cuda()
         want = oracle.stencil(g, 13) if rank == 0 else None
         for overlap in (1, 0):
-            for fuse in (1, 2):
+            for fuse in (1, 2, 4, 12):
                 stencil.set_tuning(overlap=overlap)
                 stencil.set_fusion(steps_per_pass=fuse)
                 res = stencil.run(comm, t.clone(), 13, PX, PY)
