@@ -43,6 +43,8 @@ def lib_path(variant: str = "") -> str:
     """release: _build/libsmi_amd.so; "debug": bounds-checked diagnostic build."""
     if variant == "debug":
         return os.path.join(OUT_DIR, "debug", "libsmi_amd_debug.so")
+    if variant == "rehearsal":
+        return os.path.join(OUT_DIR, "rehearsal", "libsmi_amd_rehearsal.so")
     return LIB
 
 
@@ -62,7 +64,8 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
         return lib
     out_dir = os.path.dirname(lib)
     os.makedirs(out_dir, exist_ok=True)
-    flags = CXXFLAGS + (["-DSMI_BOUNDS_CHECK"] if variant == "debug" else [])
+    flags = CXXFLAGS + {"debug": ["-DSMI_BOUNDS_CHECK"],
+                        "rehearsal": ["-DSMI_LOOPBACK_REHEARSAL"]}.get(variant, [])
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     objs = []
     procs = []
@@ -91,4 +94,4 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True,
-                variant="debug" if "--debug" in sys.argv else ""))
+                variant="debug" if "--debug" in sys.argv else ("rehearsal" if "--rehearsal" in sys.argv else "")))

@@ -69,6 +69,7 @@ struct Tuning {
     int ht2 = 8;        // rows per wave (two-step sweep)
     int u2 = 8;         // rows in flight per batch (two-step sweep)
     int htk = 0;        // rows per wave (K-step sweep, K >= 4); 0 = one round of resident waves
+    int rounds_multi = 3;  // K-step interior in multi-rank runs: rounds of resident waves
     int uk = 3;         // rows per load batch (K-step sweep: fixed at 3, the slot ring period)
 };
 extern Tuning g_tune;

@@ -5,6 +5,8 @@
 // Convert{Send,Receive}{Top,Bottom,Left,Right} kernels of
 // examples/kernels/stencil_smi.cl:236-386, whose per-element SMI_Push/SMI_Pop
 // streams become one transport group of bulk sends/receives per exchange.
+#include <cstdlib>
+
 #include "stencil_common.h"
 
 namespace smi {
@@ -213,6 +215,17 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     if (nb.top >= 0 && nb.right >= 0) nb.tr = (ipx - 1) * py + ipy + 1;
     if (nb.bottom >= 0 && nb.left >= 0) nb.bl = (ipx + 1) * py + ipy - 1;
     if (nb.bottom >= 0 && nb.right >= 0) nb.br = (ipx + 1) * py + ipy + 1;
+#ifdef SMI_LOOPBACK_REHEARSAL
+    // Timing-rehearsal build only (never the product library; built by
+    // `smi_amd/build.py --rehearsal`, driven by tools/rehearsal.py): with
+    // SMI_LOOPBACK=1 a 1x1 run is its own neighbour on every side and
+    // diagonal, so one GPU replays the full per-pass work of an interior rank
+    // of a large decomposition (ring kernel, 8-way exchange through the
+    // transport, interior sweep) with the same stream schedule.  The halos
+    // then wrap around, so the numbers differ from the stencil's.
+    if (px == 1 && py == 1 && c->size == 1 && getenv("SMI_LOOPBACK"))
+        nb.top = nb.bottom = nb.left = nb.right = nb.tl = nb.tr = nb.bl = nb.br = 0;
+#endif
     const int side_nb[4] = {nb.top, nb.bottom, nb.left, nb.right};
     int side_mask = 0;
     for (int k = 0; k < 4; ++k)

@@ -259,7 +259,17 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
         case 8: waves = resident_waves<8, 3>(); break;
         default: waves = resident_waves<12, 3>(); break;
         }
-        const int per_strip = std::max(1, waves / nstrips);
+        // Single tile: one round of resident waves.  Multi-rank interior:
+        // several rounds, so that workgroups retire during the pass and the
+        // high-priority ring kernel and RCCL exchange on the comm stream are
+        // dispatched then, instead of waiting for the whole interior pass.
+        const bool single = a.gT && a.gB && a.gL && a.gR;
+        int rounds_multi = g_tune.rounds_multi;
+#ifdef SMI_LOOPBACK_REHEARSAL
+        if (const char *e = getenv("SMI_ROUNDS_MULTI")) rounds_multi = atoi(e);
+#endif
+        const int rounds = single ? 1 : std::max(1, rounds_multi);
+        const int per_strip = std::max(1, waves * rounds / nstrips);
         ht = std::max(2 * K, (out_rows + per_strip - 1) / per_strip);
     }
     const int nrb = (out_rows + ht - 1) / ht;

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Per-rank timing rehearsal of the multi-GPU stencil on ONE GPU.
+
+Loads the rehearsal build of the library (smi_amd/build.py --rehearsal,
+SMI_LOOPBACK_REHEARSAL), in which a 1x1 run with SMI_LOOPBACK=1 is its own
+neighbour on all four sides and four diagonals: the GPU then does exactly the
+per-pass work of an interior rank of a large decomposition (ring kernel,
+8-peer exchange through the transport, interior sweep on the main stream)
+with the production stream schedule.  The halos wrap around, so the values
+are not the stencil's -- timing only.  Prints ms/step next to the plain
+single-tile run, i.e. an estimate of per-GPU weak-scaling efficiency with
+an exchange that costs one device-to-device copy of the halo bytes.
+SMI_ROUNDS_MULTI (read by the rehearsal build only) sets how many rounds of
+resident waves the multi-rank interior sweep is cut into.
+usage: rehearsal.py [tile] [K...]
+"""
+import json
+import os
+import sys
+import time
+
+os.environ["SMI_LIB_VARIANT"] = "rehearsal"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import smi_amd  # noqa: E402
+from smi_amd import profiling, stencil  # noqa: E402
+
+
+def timed(comm, t, sc, steps):
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        stencil.run(comm, t, 2 * steps, 1, 1, sc)
+        s.synchronize()
+        profiling.reset()
+        profiling.enable(True)
+        t0 = time.perf_counter()
+        stencil.run(comm, t, steps, 1, 1, sc)
+        s.synchronize()
+        dt = time.perf_counter() - t0
+        profiling.enable(False)
+    return dt / steps * 1e3
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+    ks = [int(k) for k in sys.argv[2:]] or [12]
+    smi_amd.load(build_if_missing=False)
+    comm = smi_amd.LocalGroup(1).comm(0)
+    t = torch.rand((n, n), device="cuda")
+    sc = torch.empty_like(t)
+    for k in ks:
+        stencil.set_fusion(k)
+        steps = 10 * max(k, 2)
+        os.environ.pop("SMI_LOOPBACK", None)
+        alone = timed(comm, t, sc, steps)
+        for rounds in (1, 2, 3, 4, 6):
+            os.environ["SMI_ROUNDS_MULTI"] = str(rounds)
+            for ov in (1, 0):
+                stencil.set_tuning(overlap=ov)
+                os.environ["SMI_LOOPBACK"] = "1"
+                loop = timed(comm, t, sc, steps)
+                ring = profiling.read(profiling.EDGE)
+                sweep = profiling.read(profiling.SWEEPK if k >= 4 else profiling.SWEEP)
+                os.environ.pop("SMI_LOOPBACK", None)
+                print(json.dumps({"K": k, "rounds": rounds, "overlap": ov, "tile": n,
+                                  "ms_per_step_alone": round(alone, 5),
+                                  "ms_per_step_interior_rank": round(loop, 5),
+                                  "efficiency": round(alone / loop, 4),
+                                  "ring_avg_ms": round(ring[0] / max(ring[1], 1), 5),
+                                  "interior_avg_ms": round(sweep[0] / max(sweep[1], 1), 5)}), flush=True)
+    stencil.set_tuning(overlap=1)
+    os.environ.pop("SMI_ROUNDS_MULTI", None)
+    comm.finalize()
+
+
+if __name__ == "__main__":
+    main()
