@@ -25,6 +25,7 @@
 #include "smi/scatter.h"
 #include "smi/gather.h"
 #include "smi/gesummv.h"
+#include "smi/kmeans.h"
 #include "smi/profiling.h"
 
 #endif /* SMI_H */

@@ -20,7 +20,9 @@ typedef enum {
     SMI_PROF_REDUCE_FOLD = 2,
     SMI_PROF_GEMV = 3,
     SMI_PROF_STENCIL_SWEEPK = 4, /* the K-step (temporally blocked) sweep  */
-    SMI_PROF_NUM = 5
+    SMI_PROF_KMEANS_ASSIGN = 5,  /* kmeans ComputeDistance                 */
+    SMI_PROF_KMEANS_FOLD = 6,    /* kmeans per-cluster sum chains          */
+    SMI_PROF_NUM = 7
 } SMI_ProfKernel;
 
 int smi_prof_enable(int enable);

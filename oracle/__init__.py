@@ -14,6 +14,8 @@ pure-Python restatements used to pin the C code on small cases:
   dyadic rational (any summation order gives the same bits there).
 * :func:`reduce_fold_py` -- a loop restatement of the root-side reduce fold of
   ``codegen/templates/reduce.cl:42-148`` used to cross-check the C fold.
+* :func:`kmeans_reference_data` -- the kmeans_smi host's input generator
+  (``kmeans_data.cpp``, same libstdc++ engine and distributions).
 
 Parity status per path is recorded in DESIGN.md ("Oracle").
 """
@@ -47,10 +49,13 @@ NP_DTYPE = {
 SHIFT_REG = {SMI_DOUBLE: 4, SMI_FLOAT: 4, SMI_INT: 1, SMI_SHORT: 1, SMI_CHAR: 1}
 
 
+_SOURCES = ("smi_oracle.c", "kmeans_data.cpp", "Makefile")
+
+
 def build(force: bool = False) -> str:
-    """Compile smi_oracle.c with the committed Makefile (gcc)."""
-    if force or not os.path.exists(_LIB_PATH) or (
-        os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "smi_oracle.c"))
+    """Compile smi_oracle.c + kmeans_data.cpp with the committed Makefile."""
+    if force or not os.path.exists(_LIB_PATH) or any(
+        os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, f)) for f in _SOURCES
     ):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
@@ -67,8 +72,16 @@ def lib() -> ctypes.CDLL:
         _lib.oracle_stencil_decomposed.argtypes = [P, P, I, I, I, I, I]
         _lib.oracle_reduce.argtypes = [P, P, I, ctypes.c_long, I, I, P]
         _lib.oracle_gesummv.argtypes = [P, P, P, P, I, I, ctypes.c_float, ctypes.c_float, I]
+        L = ctypes.c_long
+        _lib.oracle_kmeans_assign.argtypes = [P, L, I, P, I, I, P]
+        _lib.oracle_kmeans_accumulate.argtypes = [P, L, I, P, I, P, P]
+        _lib.oracle_kmeans.argtypes = [P, L, I, I, I, I, P, I]
+        _lib.oracle_kmeans_reference_data.argtypes = [I, I, I, P, P, P]
+        _lib.oracle_minstd_rand0_10000.argtypes = []
+        _lib.oracle_minstd_rand0_10000.restype = ctypes.c_ulong
         for f in ("oracle_stencil", "oracle_stencil_decomposed", "oracle_reduce",
-                  "oracle_gesummv", "oracle_max_threads"):
+                  "oracle_gesummv", "oracle_max_threads", "oracle_kmeans_assign",
+                  "oracle_kmeans_accumulate", "oracle_kmeans", "oracle_kmeans_reference_data"):
             getattr(_lib, f).restype = ctypes.c_int
     return _lib
 
@@ -243,3 +256,56 @@ def gesummv_reference_check(result: np.ndarray, A, B, x, alpha, beta) -> bool:
 
 def max_threads() -> int:
     return int(lib().oracle_max_threads())
+
+
+# ----------------------------------------------------------------- kmeans --
+def kmeans_assign(points: np.ndarray, centroids: np.ndarray, width: int = 16) -> np.ndarray:
+    """ComputeDistance (examples/kernels/kmeans_smi.cl:54-85), W = width."""
+    p = np.ascontiguousarray(points, dtype=np.float32)
+    c = np.ascontiguousarray(centroids, dtype=np.float32)
+    idx = np.empty(p.shape[0], dtype=np.int32)
+    rc = lib().oracle_kmeans_assign(_ptr(p), p.shape[0], p.shape[1], _ptr(c), c.shape[0], width, _ptr(idx))
+    if rc:
+        raise ValueError(f"oracle_kmeans_assign rc={rc}")
+    return idx
+
+
+def kmeans_accumulate(points: np.ndarray, assignment: np.ndarray, clusters: int):
+    """ComputeMeans accumulation (kmeans_smi.cl:98-127): (sums, counts)."""
+    p = np.ascontiguousarray(points, dtype=np.float32)
+    a = np.ascontiguousarray(assignment, dtype=np.int32)
+    sums = np.empty((clusters, p.shape[1]), dtype=np.float32)
+    counts = np.empty(clusters, dtype=np.int32)
+    rc = lib().oracle_kmeans_accumulate(_ptr(p), p.shape[0], p.shape[1], _ptr(a), clusters, _ptr(sums),
+                                        _ptr(counts))
+    if rc:
+        raise ValueError(f"oracle_kmeans_accumulate rc={rc}")
+    return sums, counts
+
+
+def kmeans(points: np.ndarray, centroids: np.ndarray, iterations: int, ranks: int = 1,
+           width: int = 16) -> np.ndarray:
+    """The kmeans_smi program over `ranks` ranks; returns the final centroids."""
+    p = np.ascontiguousarray(points, dtype=np.float32)
+    c = np.array(centroids, dtype=np.float32, order="C", copy=True)
+    rc = lib().oracle_kmeans(_ptr(p), p.shape[0], ranks, p.shape[1], c.shape[0], width, _ptr(c), iterations)
+    if rc:
+        raise ValueError(f"oracle_kmeans rc={rc}")
+    return c
+
+
+def kmeans_reference_data(num_points: int, clusters: int = 8, dims: int = 64):
+    """(means, points, initial centroids) exactly as the reference host
+    generates them on rank 0 (examples/host/kmeans_smi.cpp:96-147)."""
+    means = np.empty((clusters, dims), dtype=np.float32)
+    pts = np.empty((num_points, dims), dtype=np.float32)
+    cen = np.empty((clusters, dims), dtype=np.float32)
+    rc = lib().oracle_kmeans_reference_data(num_points, clusters, dims, _ptr(means), _ptr(pts), _ptr(cen))
+    if rc:
+        raise ValueError("the reference host would copy a centroid from past the end of its input "
+                         "(uniform_int_distribution(0, num_points) is inclusive, kmeans_smi.cpp:141)")
+    return means, pts, cen
+
+
+def minstd_rand0_10000() -> int:
+    return int(lib().oracle_minstd_rand0_10000())

@@ -22,9 +22,15 @@
  *     pinned by any reference fixture (none exists).
  *   - gesummv: pinned by the reference host check (rel. err < 1e-4 vs two
  *     sgemv calls, examples/host/gesummv_smi.cpp:40-46,299-313).
+ *   - kmeans: the reference has no check or fixture for kmeans_smi; the
+ *     restatement is pinned by independent numpy/Python restatements of
+ *     kmeans_smi.cl (tests/test_oracle.py) and runs on the reference host's
+ *     own input (kmeans_data.cpp, libstdc++ engine pinned by the standard's
+ *     minstd_rand0 check value) -- parity unpinned beyond that.
  */
 #include <float.h>
 #include <limits.h>
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -373,4 +379,102 @@ int oracle_max_threads(void) {
 #else
     return 1;
 #endif
+}
+
+/* ------------------------------------------------------------------------ */
+/* kmeans                                                                    */
+/* ------------------------------------------------------------------------ */
+
+/* ComputeDistance, examples/kernels/kmeans_smi.cl:54-85, for the vector width
+ * W of the build (VTYPE = float<W>, examples/include/kmeans.h.in; W = 16 in
+ * the reference build, examples/CMakeLists.txt:5).  Restated literally: for
+ * every W-wide vector the unrolled loop :68-71 ASSIGNS
+ * dist_contribution = diff * diff for w = 0..W-1, so :72 adds the last
+ * lane's; the argmin starts at +INFINITY and takes k only on a strict <. */
+int oracle_kmeans_assign(const float *pts, long n, int dims, const float *cen, int clusters, int width,
+                         int *idx) {
+    if (n < 0 || dims <= 0 || clusters <= 0 || width <= 0 || dims % width) return -1;
+    const int vecs = dims / width;
+    for (long p = 0; p < n; ++p) {
+        const float *x = pts + (size_t)p * dims;
+        float min_dist = INFINITY;
+        int min_idx = 0;
+        for (int k = 0; k < clusters; ++k) {
+            const float *c = cen + (size_t)k * dims;
+            float dist = 0.0f;
+            for (int d = 0; d < vecs; ++d) {
+                float dist_contribution = 0.0f;
+                for (int w = 0; w < width; ++w) {
+                    const float diff = x[d * width + w] - c[d * width + w];
+                    dist_contribution = diff * diff;
+                }
+                dist += dist_contribution;
+            }
+            if (dist < min_dist) {
+                min_dist = dist;
+                min_idx = k;
+            }
+        }
+        idx[p] = min_idx;
+    }
+    return 0;
+}
+
+/* ComputeMeans accumulation, kmeans_smi.cl:98-127, literally: every point
+ * adds its vector to its own cluster's sums and +0 to every other cluster's,
+ * in point order (`means[d][k] += (index == k) ? dims : 0`); counts alike. */
+int oracle_kmeans_accumulate(const float *pts, long n, int dims, const int *idx, int clusters, float *sums,
+                             int *counts) {
+    if (n < 0 || dims <= 0 || clusters <= 0) return -1;
+    for (size_t i = 0; i < (size_t)clusters * dims; ++i) sums[i] = 0.0f;
+    for (int k = 0; k < clusters; ++k) counts[k] = 0;
+    for (long p = 0; p < n; ++p) {
+        const int index = idx[p];
+        for (int d = 0; d < dims; ++d) {
+            const float v = pts[(size_t)p * dims + d];
+            for (int k = 0; k < clusters; ++k) {
+                sums[(size_t)k * dims + d] += (index == k) ? v : 0.0f;
+                if (d == 0) counts[k] += (index == k) ? 1 : 0;
+            }
+        }
+    }
+    return 0;
+}
+
+/* The kmeans_smi program over `ranks` ranks: the points split in rank order
+ * as by the host's MPI_Scatter (kmeans_smi.cpp:165-166), every rank starting
+ * from the same centroids (MPI_Bcast, :164).  Each iteration: assign and
+ * accumulate per rank; SMI_Reduce of the sums (fp32 add, port 0) and counts
+ * (int add, port 2) to rank 0 through the support-kernel fold above
+ * (canonical rank order); SMI_Bcast (ports 1, 3); centroid =
+ * sum / (float)count (kmeans_smi.cl:196-205). */
+int oracle_kmeans(const float *pts, long n_total, int ranks, int dims, int clusters, int width, float *centroids,
+                  int iterations) {
+    if (ranks <= 0 || n_total < 0 || n_total % ranks || dims <= 0 || width <= 0 || dims % width) return -1;
+    const long per = n_total / ranks;
+    const size_t kd = (size_t)clusters * dims;
+    int *idx = malloc(((size_t)per + 1) * sizeof(int));
+    float *sums = malloc((size_t)ranks * kd * sizeof(float));
+    int *counts = malloc((size_t)ranks * clusters * sizeof(int));
+    float *rs = malloc(kd * sizeof(float));
+    int *rc = malloc((size_t)clusters * sizeof(int));
+    int err = (!idx || !sums || !counts || !rs || !rc) ? -4 : 0;
+    for (int it = 0; it < iterations && !err; ++it) {
+        for (int r = 0; r < ranks && !err; ++r) {
+            const float *mine = pts + (size_t)r * per * dims;
+            err = oracle_kmeans_assign(mine, per, dims, centroids, clusters, width, idx);
+            if (!err)
+                err = oracle_kmeans_accumulate(mine, per, dims, idx, clusters, sums + (size_t)r * kd,
+                                               counts + (size_t)r * clusters);
+        }
+        if (!err) err = oracle_reduce(sums, rs, ranks, (long)kd, OR_FLOAT, OR_ADD, NULL);
+        if (!err) err = oracle_reduce(counts, rc, ranks, clusters, OR_INT, OR_ADD, NULL);
+        for (size_t i = 0; i < kd && !err; ++i) centroids[i] = rs[i] / (float)rc[i / dims];
+    }
+    free(idx);
+    free(sums);
+    free(counts);
+    free(rs);
+    free(rc);
+    return err;
 }

@@ -29,7 +29,8 @@ SMI_ADD, SMI_MAX, SMI_MIN = 0, 1, 2
 # include/smi/stencil.h
 SIDE_COPY, SIDE_HALO, SIDE_SKIP = 0, 1, 2
 # include/smi/profiling.h
-PROF_STENCIL_SWEEP, PROF_STENCIL_EDGE, PROF_REDUCE_FOLD, PROF_GEMV, PROF_STENCIL_SWEEPK = 0, 1, 2, 3, 4
+(PROF_STENCIL_SWEEP, PROF_STENCIL_EDGE, PROF_REDUCE_FOLD, PROF_GEMV, PROF_STENCIL_SWEEPK, PROF_KMEANS_ASSIGN,
+ PROF_KMEANS_FOLD) = 0, 1, 2, 3, 4, 5, 6
 
 
 class SMIError(RuntimeError):
@@ -69,6 +70,9 @@ SIGNATURES = {
     "smi_gather": (I, [SMI_Comm, P, P, SZ, I, I, I, P]),
     "smi_gemv_rows": (I, [P, P, P, P, I, I, I, F, F, P]),
     "smi_gesummv": (I, [SMI_Comm, P, P, P, P, I, I, F, F, I, P]),
+    "smi_kmeans_assign": (I, [P, I, I, P, I, I, P, P]),
+    "smi_kmeans_accumulate": (I, [P, I, I, P, I, P, P, P]),
+    "smi_kmeans": (I, [SMI_Comm, P, I, I, I, I, P, I, P]),
     "smi_prof_enable": (I, [I]),
     "smi_prof_reset": (I, []),
     "smi_prof_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),

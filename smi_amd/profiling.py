@@ -10,6 +10,8 @@ EDGE = _lib.PROF_STENCIL_EDGE
 REDUCE_FOLD = _lib.PROF_REDUCE_FOLD
 GEMV = _lib.PROF_GEMV
 SWEEPK = _lib.PROF_STENCIL_SWEEPK
+KMEANS_ASSIGN = _lib.PROF_KMEANS_ASSIGN
+KMEANS_FOLD = _lib.PROF_KMEANS_FOLD
 
 
 def enable(on: bool = True) -> None:

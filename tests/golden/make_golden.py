@@ -47,6 +47,16 @@ def main():
         red.append(dict(n=n, seed=100 + n, inputs=c.tolist(),
                         fp32_add=o.reduce(c, o.SMI_FLOAT, o.SMI_ADD).view(np.uint32).tolist()))
     out["reduce"] = red
+    # kmeans_smi on the reference host's own input (its generator, 8 clusters
+    # x 64 dims, W = 16, 8 ranks as SMI_KMEANS_RANKS) and a W = 1 variant
+    km = []
+    for case in (dict(num_points=2048, ranks=8, width=16, iterations=10),
+                 dict(num_points=1536, ranks=3, width=1, iterations=6)):
+        _, pts, cen = o.kmeans_reference_data(case["num_points"], 8, 64)
+        c = o.kmeans(pts, cen, case["iterations"], ranks=case["ranks"], width=case["width"])
+        km.append(dict(case, clusters=8, dims=64, sha256=hashlib.sha256(c.tobytes()).hexdigest(),
+                       centroid0=c[0].tolist()))
+    out["kmeans"] = km
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", os.path.join(HERE, "golden.json"))

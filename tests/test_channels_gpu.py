@@ -8,6 +8,10 @@ Known-answer tests replayed from the reference's own suites:
   reduce    test/reduce/reduce.cl:7-172, lengths {1,128,300} x roots {1,4,7}
   scatter   test/scatter/scatter.cl (root scatters i, rank r checks r*N+i)
   gather    test/gather/gather.cl (rank r sends r; root sees 0..n-1 in order)
+  mixed     test/mixed/mixed.cl:11-35 (p2p pipeline, then a bcast)
+  balanced  test/balanced_routing/balanced_routing.cl (two-port pipeline,
+            two concurrent bcasts; lengths {2,8,10000}, roots {0,4,5},
+            test_balanced_routing.cpp:75,105-107)
 plus port demultiplexing and push-before-pop buffering, and the bulk
 smi_scatter / smi_gather on device buffers.
 """
@@ -203,3 +207,74 @@ def test_bulk_scatter_gather(gpu, n):
             return ok
 
     assert all(group(n, fn))
+
+
+@pytest.mark.parametrize("start", [0, 41])
+def test_mixed_reference_kat(gpu, start):
+    """test/mixed/mixed.cl:11-35: rank r pops from r-1, adds one, pushes to
+    r+1; the last rank then broadcasts on port 1 -- all end with start+n-1."""
+    from smi_amd import channels as ch
+
+    def fn(comm):
+        r, n = comm.rank, comm.size
+        data = start
+        if r > 0:
+            data = int(ch.open_receive_channel(1, INT, r - 1, 0, comm).pop()) + 1
+        if r < n - 1:
+            ch.open_send_channel(1, INT, r + 1, 0, comm).push(data)
+        final = data if r == n - 1 else 0
+        return int(ch.BChannel(1, INT, 1, n - 1, comm).bcast(final))
+
+    assert group(8, fn) == [start + 7] * 8
+
+
+@pytest.mark.parametrize("N", [2, 8, 10000])
+def test_balanced_routing_pipeline_kat(gpu, N):
+    """balanced_routing.cl:8-48: two channels per direction along the rank
+    pipeline; the last rank sees i + n - 1 and i + n."""
+    from smi_amd import channels as ch
+
+    def fn(comm):
+        r, n = comm.rank, comm.size
+        if r > 0:
+            r1 = ch.open_receive_channel(N, INT, r - 1, 0, comm)
+            r2 = ch.open_receive_channel(N, INT, r - 1, 1, comm)
+        if r < n - 1:
+            s1 = ch.open_send_channel(N, INT, r + 1, 0, comm)
+            s2 = ch.open_send_channel(N, INT, r + 1, 1, comm)
+        ok, e1, e2 = True, n - 1, n
+        for i in range(N):
+            if r > 0:
+                d1, d2 = int(r1.pop()) + 1, int(r2.pop()) + 1
+            else:
+                d1, d2 = i, i + 1
+            if r < n - 1:
+                s1.push(d1)
+                s2.push(d2)
+            else:
+                ok &= d1 == e1 and d2 == e2
+                e1 += 1
+                e2 += 1
+        return ok
+
+    assert all(group(8, fn))
+
+
+@pytest.mark.parametrize("N", [2, 8, 10000])
+@pytest.mark.parametrize("root", [0, 4, 5])
+def test_balanced_routing_broadcast_kat(gpu, N, root):
+    """balanced_routing.cl:51-69: two broadcasts (ports 2, 3) interleaved
+    element by element."""
+    from smi_amd import channels as ch
+
+    def fn(comm):
+        b1 = ch.BChannel(N, INT, 2, root, comm)
+        b2 = ch.BChannel(N, INT, 3, root, comm)
+        ok = True
+        for i in range(N):
+            a = b1.bcast(i if comm.rank == root else -1)
+            b = b2.bcast(i if comm.rank == root else -1)
+            ok &= a == i and b == i
+        return ok
+
+    assert all(group(8, fn))

@@ -145,6 +145,10 @@ def test_golden_fixtures_reproduce():
         assert hashlib.sha256(out.tobytes()).hexdigest() == case["sha256"], case
     arr = np.load(os.path.join(GOLDEN, "stencil_uniform_64x96_T16.npy"))
     assert np.array_equal(o.stencil(o.init_uniform(64, 96, seed=42), 16), arr)
+    for case in gold["kmeans"]:
+        _, pts, cen = o.kmeans_reference_data(case["num_points"], case["clusters"], case["dims"])
+        c = o.kmeans(pts, cen, case["iterations"], ranks=case["ranks"], width=case["width"])
+        assert hashlib.sha256(c.tobytes()).hexdigest() == case["sha256"], case
 
 
 # --------------------------------------------------------------- gesummv --
@@ -184,3 +188,94 @@ def test_gesummv_fold_restatement():
     want = np.float32(fold(a, 1.5) + fold(b, 0.5))
     got = o.gesummv(a[None, :], b[None, :], x, 1.5, 0.5)[0]
     assert got.view(np.uint32) == want.view(np.uint32)
+
+
+# ---------------------------------------------------------------- kmeans --
+def test_kmeans_generator_engine_kat():
+    """The reference host seeds std::default_random_engine (libstdc++:
+    minstd_rand0); the C++ standard's check value pins the engine."""
+    assert o.minstd_rand0_10000() == 1043618065
+
+
+def test_kmeans_reference_data():
+    """kmeans_smi.cpp:99-147: means in [-5, 5), point i ~ N(mean_{i%K}, 1),
+    initial centroids copied from input points."""
+    means, pts, cen = o.kmeans_reference_data(2048, 8, 64)
+    assert means.min() >= -5 and means.max() < 5
+    d = pts.reshape(256, 8, 64) - means[None]
+    assert abs(float(d.mean())) < 0.02 and abs(float(d.std()) - 1) < 0.02
+    rows = {r.tobytes() for r in pts}
+    assert all(c.tobytes() in rows for c in cen)
+
+
+def _assign_numpy(pts, cen, width):
+    """Vectorised restatement of kmeans_smi.cl:54-85: the last lane of each
+    W-wide vector, fp32 mul then add, strict < from +inf."""
+    f = np.float32
+    xs, cs = pts[:, width - 1::width], cen[:, width - 1::width]
+    dist = np.zeros((len(pts), len(cen)), f)
+    for j in range(xs.shape[1]):
+        diff = (xs[:, None, j] - cs[None, :, j]).astype(f)
+        dist = (dist + (diff * diff).astype(f)).astype(f)
+    best = np.zeros(len(pts), np.int32)
+    mind = np.full(len(pts), np.inf, f)
+    for k in range(len(cen)):
+        upd = dist[:, k] < mind
+        best[upd] = k
+        mind[upd] = dist[upd, k]
+    return best
+
+
+@pytest.mark.parametrize("width", [1, 4, 16])
+def test_kmeans_assign_restatement(width):
+    rng = np.random.default_rng(width)
+    pts = rng.standard_normal((500, 64), dtype=np.float32)
+    cen = rng.standard_normal((8, 64), dtype=np.float32)
+    cen[3] = cen[1]                      # tie: the lower index wins
+    pts[7] = np.nan                      # all-NaN distances: cluster 0
+    got = o.kmeans_assign(pts, cen, width)
+    assert np.array_equal(got, _assign_numpy(pts, cen, width))
+    assert got[7] == 0 and not np.any(got == 3)
+
+
+def test_kmeans_accumulate_restatement():
+    """Sequential Python restatement of the per-cluster chains; the form that
+    skips other clusters' points (the GPU's) gives the same bits as the
+    literal `+= (index == k) ? x : 0` of kmeans_smi.cl:122."""
+    rng = np.random.default_rng(4)
+    n, dims, K = 300, 5, 4
+    pts = (rng.standard_normal((n, dims)) * 100).astype(np.float32)
+    pts[::17] *= -1
+    pts[5, 2] = -0.0
+    asg = rng.integers(-1, K + 1, n).astype(np.int32)   # -1 and K belong to no cluster
+    f = np.float32
+    want = np.zeros((K, dims), f)
+    for p in range(n):
+        if 0 <= asg[p] < K:
+            want[asg[p]] = (want[asg[p]] + pts[p]).astype(f)
+    sums, counts = o.kmeans_accumulate(pts, asg, K)
+    assert np.array_equal(sums.view(np.uint32), want.view(np.uint32))
+    assert np.array_equal(counts, np.array([(asg == k).sum() for k in range(K)]))
+
+
+@pytest.mark.parametrize("ranks", [1, 4, 8])
+def test_kmeans_program_composition(ranks):
+    """oracle_kmeans = per-rank assign + accumulate, the reduce fold over the
+    ranks, and IEEE division -- composed here from the pieces."""
+    _, pts, cen = o.kmeans_reference_data(1024, 8, 64)
+    c = cen.copy()
+    per = len(pts) // ranks
+    for _ in range(3):
+        s, n = [], []
+        for r in range(ranks):
+            mine = pts[r * per:(r + 1) * per]
+            a, b = o.kmeans_accumulate(mine, o.kmeans_assign(mine, c, 16), 8)
+            s.append(a.ravel())
+            n.append(b)
+        rs = o.reduce(np.stack(s), o.SMI_FLOAT, o.SMI_ADD).reshape(8, 64)
+        rc = o.reduce(np.stack(n), o.SMI_INT, o.SMI_ADD)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            c = (rs / rc.astype(np.float32)[:, None]).astype(np.float32)
+    want = o.kmeans(pts, cen, 3, ranks=ranks, width=16)
+    assert np.array_equal(np.isnan(c), np.isnan(want))
+    assert np.array_equal(c[~np.isnan(c)], want[~np.isnan(want)])

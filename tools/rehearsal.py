@@ -27,7 +27,14 @@ import smi_amd  # noqa: E402
 from smi_amd import profiling, stencil  # noqa: E402
 
 
-def timed(comm, t, sc, steps):
+def timed(comm, t, sc, steps, reps=3):
+    """min over `reps` runs of ms per step (the in-process transport creates
+    and retires HIP events per message: occasional host stalls that RCCL
+    does not have)"""
+    return min(_timed(comm, t, sc, steps) for _ in range(reps))
+
+
+def _timed(comm, t, sc, steps):
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         stencil.run(comm, t, 2 * steps, 1, 1, sc)
@@ -54,7 +61,7 @@ def main():
         steps = 10 * max(k, 2)
         os.environ.pop("SMI_LOOPBACK", None)
         alone = timed(comm, t, sc, steps)
-        for rounds in (1, 2, 3, 4, 6):
+        for rounds in (2, 3, 4, 6):
             os.environ["SMI_ROUNDS_MULTI"] = str(rounds)
             for ov in (1, 0):
                 stencil.set_tuning(overlap=ov)
