@@ -24,6 +24,13 @@ The JSON line also carries:
   cpu_baseline  -- the oracle's C restatement of the reference stencil
                    (OpenMP) timed on this host on a bounded sample (rank 0,
                    N=1 only)
+  halo          -- (N>1) xGMI bytes per step of the halo exchange and the
+                   per-link rate the measured step time demands
+  aux           -- measured after the timed stencil region (skip: --no-aux):
+                   gesummv 32768^2 row-sharded over the N GPUs (BASELINE
+                   config 5) and, for N>1, SMI_Reduce int32/fp32 and SMI_Bcast
+                   at 4 KiB-256 MiB (config 4) with algbw vs the xGMI bound;
+                   bounded by a watchdog so the stencil line always prints
 """
 from __future__ import annotations
 
@@ -31,6 +38,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -43,6 +51,10 @@ BYTES_PER_CELL = 8             # one fp32 read + one fp32 write per cell per ste
 TILE = 8192                    # per-GPU tile edge (BASELINE config 2 / weak scaling)
 DECOMP = {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_stencil_sweep.json")
+XGMI_LINK_GBS = 153.6          # MI355X Infinity Fabric: 7 links x 153.6 GB/s per GPU
+GESUMMV_N = 32768              # BASELINE config 5
+COLL_BYTES = (4 << 10, 1 << 20, 64 << 20, 256 << 20)   # BASELINE config 4 span
+AUX_BUDGET_S = 120.0           # watchdog on the auxiliary measurements
 
 
 def decomposition(n: int) -> tuple[int, int]:
@@ -92,6 +104,124 @@ def pmc_traffic(cells: int, steps_per_launch: int) -> float | None:
     return None
 
 
+def halo_report(PX: int, PY: int, X: int, Y: int, K: int, ms_per_step: float) -> dict:
+    """xGMI traffic of the halo exchange for the busiest rank: per K-step pass
+    a rank sends K rows of Y fp32 to each vertical neighbour, K columns of X
+    fp32 to each horizontal neighbour and a KxK block to each diagonal
+    neighbour (stencil_smi.cl:183-224 streams the same rows/columns one step
+    at a time).  Every neighbour is its own xGMI link, so the per-link rate
+    is the largest single-neighbour payload over the step time."""
+    best = None
+    for ipx in range(PX):
+        for ipy in range(PY):
+            nv = (ipx > 0) + (ipx < PX - 1)
+            nh = (ipy > 0) + (ipy < PY - 1)
+            nd = sum(1 for dx in (-1, 1) for dy in (-1, 1)
+                     if 0 <= ipx + dx < PX and 0 <= ipy + dy < PY)
+            b = 4 * (nv * Y + nh * X) + 4 * nd * K  # per step (KxK block / K steps)
+            if best is None or b > best[0]:
+                best = (b, nv, nh, nd)
+    b, nv, nh, nd = best
+    link_b = 4 * max(Y if nv else 0, X if nh else 0)
+    link_rate = link_b / (ms_per_step * 1e-3) / 1e9
+    return {
+        "bytes_per_step_busiest_rank": b,
+        "neighbours": {"vertical": nv, "horizontal": nh, "diagonal": nd},
+        "link_GBs_needed": round(link_rate, 2),
+        "link_peak_GBs": XGMI_LINK_GBS,
+        "link_frac": round(link_rate / XGMI_LINK_GBS, 4),
+        "note": "per-link halo rate the measured step time demands; the exchange is latency-bound "
+                "(K rows/columns per pass), hidden behind the interior sweep",
+    }
+
+
+def _timed(fn, iters: int, barrier, world: int) -> float:
+    """Seconds per call: one untimed call, then `iters` calls bracketed by a
+    barrier + device sync; max over ranks."""
+    import torch
+    import torch.distributed as dist
+    fn()
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    barrier()
+    dt = (time.perf_counter() - t0) / iters
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t[0])
+    return dt
+
+
+def aux_gesummv(comm, world: int, rank: int, stream, barrier) -> dict:
+    """BASELINE config 5: y = alpha*A*x + beta*B*x, 32768^2 fp32, rows sharded
+    over the ranks (strong scaling), y chunks gathered on rank 0
+    (gesummv_rank0.cl:53-203).  Algorithmic bytes 4*(2*N*M + M + N)."""
+    import torch
+    from smi_amd import gesummv
+    n = m = GESUMMV_N
+    r0, r1 = gesummv.row_range(n, world, rank)
+    gen = torch.Generator(device="cuda").manual_seed(77 + rank)
+    A = torch.rand((r1 - r0, m), generator=gen, device="cuda") * 2 - 1
+    B = torch.rand((r1 - r0, m), generator=gen, device="cuda") * 2 - 1
+    x = torch.ones(m, device="cuda")
+    y = torch.empty(n, device="cuda") if rank == 0 else None
+    torch.cuda.synchronize()
+
+    def call():
+        gesummv.gesummv(comm, A, B, x, n, 1.5, 0.5, y=y, root=0, stream=stream)
+
+    with torch.cuda.stream(stream):
+        dt = _timed(call, 10, barrier, world)
+    del A, B
+    algo = 4 * (2 * n * m + m + n)
+    gbs = algo / dt / 1e9
+    return {"workload": f"gesummv {n}x{m} fp32, {world}-way row shard, y gathered on rank 0",
+            "ms": round(dt * 1e3, 4), "GBs": round(gbs, 1),
+            "hbm_frac": round(gbs / (HBM_PEAK_GBS * world), 4)}
+
+
+def aux_collectives(comm, world: int, rank: int, stream, barrier) -> list:
+    """BASELINE config 4: SMI_Reduce (int32 + fp32 add) and SMI_Bcast, 4 KiB -
+    256 MiB per rank.  algbw = message bytes / time; the xGMI bound for the
+    owner-chunk reduce (and scatter + all-gather bcast) is n*B_link/2: each
+    link carries 2*N/n bytes per direction."""
+    import torch
+    from smi_amd import collectives
+    out = []
+    root = world - 1
+    for nbytes in COLL_BYTES:
+        count = nbytes // 4
+        iters = 20 if nbytes <= (1 << 20) else 5
+        snd_i = torch.full((count,), rank + 1, dtype=torch.int32, device="cuda")
+        snd_f = torch.rand(count, device="cuda")
+        rcv = torch.empty(count, dtype=torch.float32, device="cuda") if rank == root else None
+        rcv_i = torch.empty(count, dtype=torch.int32, device="cuda") if rank == root else None
+        buf = torch.rand(count, device="cuda")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(stream):
+            t_ri = _timed(lambda: collectives.reduce(comm, snd_i, rcv_i, "add", root=root, stream=stream),
+                          iters, barrier, world)
+            t_rf = _timed(lambda: collectives.reduce(comm, snd_f, rcv, "add", root=root, stream=stream),
+                          iters, barrier, world)
+            t_b = _timed(lambda: collectives.bcast(comm, buf, root=0, stream=stream), iters, barrier, world)
+        ok = True
+        if rank == root:  # KAT: sum of (rank + 1) = n(n+1)/2 (microbenchmarks/kernels/reduce.cl:13-24)
+            ok = bool((rcv_i == world * (world + 1) // 2).all().item())
+        bound = world * XGMI_LINK_GBS / 2
+        for op, t in (("reduce_i32_add", t_ri), ("reduce_f32_add", t_rf), ("bcast_f32", t_b)):
+            gbs = nbytes / t / 1e9
+            out.append({"op": op, "bytes": nbytes, "us": round(t * 1e6, 1), "algbw_GBs": round(gbs, 2),
+                        "xgmi_bound_GBs": bound, "xgmi_frac": round(gbs / bound, 4)})
+        if not ok:
+            out.append({"op": "reduce_i32_add", "bytes": nbytes, "error": "KAT mismatch"})
+        del snd_i, snd_f, rcv, rcv_i, buf
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -99,6 +229,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--tile", type=int, default=TILE)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-aux", action="store_true",
+                    help="skip the gesummv / reduce / bcast lines measured after the timed stencil region")
     args = ap.parse_args()
 
     import torch
@@ -237,13 +369,44 @@ def main() -> None:
         out["roofline"]["hbm_frac"] = round(hbm / HBM_PEAK_GBS, 4)
     if edge_n:
         out["roofline"]["edge_kernel_avg_ms"] = round(edge_ms / edge_n, 5)
+    if world > 1:
+        out["halo"] = halo_report(PX, PY, X, Y, spl if deep else 1, elapsed / args.steps * 1e3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+
+    # Auxiliary lines (BASELINE configs 4 and 5), measured after the timed
+    # stencil region.  A watchdog bounds them: if they do not finish, rank 0
+    # still prints the stencil line and every rank exits.
+    printed = threading.Lock()
+
+    def emit(o):
+        if rank == 0 and printed.acquire(blocking=False):
+            print(json.dumps(o), flush=True)
+
+    def watchdog():
+        o = dict(out)
+        o["aux"] = {"error": f"auxiliary measurements exceeded {AUX_BUDGET_S:.0f} s"}
+        emit(o)
+        os._exit(0)
+
+    if not args.no_aux:
+        timer = threading.Timer(AUX_BUDGET_S, watchdog)
+        timer.daemon = True
+        timer.start()
+        aux = {}
+        try:
+            aux["gesummv"] = aux_gesummv(comm, world, rank, stream, barrier)
+            if world > 1:
+                aux["collectives"] = aux_collectives(comm, world, rank, stream, barrier)
+        except Exception as e:  # report, never lose the stencil line
+            aux["error"] = f"{type(e).__name__}: {e}"
+        out["aux"] = aux
+    emit(out)
     comm.finalize()
     if world > 1:
         dist.destroy_process_group()
+    if not args.no_aux:
+        timer.cancel()  # after teardown: a wedged finalize is bounded too
 
 
 if __name__ == "__main__":
