@@ -61,10 +61,10 @@ def test_bench_decomposition():
 
 def test_bench_halo_report_counts_neighbours():
     import bench
-    # 2x4: an inner-column rank has 1 vertical, 2 horizontal, 3 diagonal neighbours
+    # 2x4: an inner-column rank has 1 vertical, 2 horizontal, 2 diagonal neighbours
     h = bench.halo_report(2, 4, 8192, 8192, 12, 0.02)
-    assert h["neighbours"] == {"vertical": 1, "horizontal": 2, "diagonal": 3}
-    assert h["bytes_per_step_busiest_rank"] == 4 * (8192 + 2 * 8192) + 4 * 3 * 12
+    assert h["neighbours"] == {"vertical": 1, "horizontal": 2, "diagonal": 2}
+    assert h["bytes_per_step_busiest_rank"] == 4 * (8192 + 2 * 8192) + 4 * 2 * 12
     # one 32 KiB column per step per link at 20 us per step
     assert abs(h["link_GBs_needed"] - 32768 / 20e-6 / 1e9) < 0.01
     h1 = bench.halo_report(1, 2, 8192, 8192, 12, 0.02)
