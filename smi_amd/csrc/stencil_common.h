@@ -69,7 +69,13 @@ struct Tuning {
     int ht2 = 8;        // rows per wave (two-step sweep)
     int u2 = 8;         // rows in flight per batch (two-step sweep)
     int htk = 0;        // rows per wave (K-step sweep, K >= 4); 0 = one round of resident waves
-    int rounds_multi = 3;  // K-step interior in multi-rank runs: rounds of resident waves
+    // K-step interior in multi-rank runs: rounds of resident waves.  One round
+    // hides the ring + a one-kernel exchange completely on the loopback
+    // rehearsal (0.997 of a lone tile), 2 rounds 0.985, 3 rounds 0.92
+    // (profiles/r01e/rehearsal_fused_exchange.log); 2 keeps a mid-pass point
+    // where workgroups retire, so the RCCL kernel of the exchange is never
+    // left without a slot until the interior ends.
+    int rounds_multi = 2;
     int uk = 3;         // rows per load batch (K-step sweep: fixed at 3, the slot ring period)
 };
 extern Tuning g_tune;
@@ -143,5 +149,8 @@ struct RingKArgs {
 };
 int launch_ringk(RingKArgs a, hipStream_t s);
 int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s);
+#ifdef SMI_LOOPBACK_REHEARSAL
+int launch_multicopy(const float *const *src, float *const *dst, const size_t *bytes, int nseg, hipStream_t s);
+#endif
 
 }  // namespace smi

@@ -159,4 +159,33 @@ int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hip
     return SMI_SUCCESS;
 }
 
+#ifdef SMI_LOOPBACK_REHEARSAL
+// Rehearsal build only: the 8-way loopback exchange as ONE copy kernel (an
+// RCCL send/recv group is one kernel launch too), so tools/rehearsal.py can
+// price the exchange without the in-process transport's per-message events.
+struct CopySegs {
+    const float4 *src[8];
+    float4 *dst[8];
+    int n4[8];
+};
+__global__ __launch_bounds__(256) void multicopy_kernel(CopySegs c, int nseg, int blocks_per_seg) {
+    const int seg = blockIdx.x / blocks_per_seg;
+    if (seg >= nseg) return;
+    const int b = blockIdx.x - seg * blocks_per_seg;
+    for (int i = b * 256 + threadIdx.x; i < c.n4[seg]; i += blocks_per_seg * 256) c.dst[seg][i] = c.src[seg][i];
+}
+int launch_multicopy(const float *const *src, float *const *dst, const size_t *bytes, int nseg, hipStream_t s) {
+    CopySegs c{};
+    for (int i = 0; i < nseg && i < 8; ++i) {
+        c.src[i] = reinterpret_cast<const float4 *>(src[i]);
+        c.dst[i] = reinterpret_cast<float4 *>(dst[i]);
+        c.n4[i] = (int)(bytes[i] / 16);
+    }
+    const int bps = 8;
+    hipLaunchKernelGGL(multicopy_kernel, dim3(bps * nseg), dim3(256), 0, s, c, nseg, bps);
+    SMI_HIP_CHECK(hipGetLastError());
+    return SMI_SUCCESS;
+}
+#endif
+
 }  // namespace smi

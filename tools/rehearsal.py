@@ -27,11 +27,11 @@ import smi_amd  # noqa: E402
 from smi_amd import profiling, stencil  # noqa: E402
 
 
-def timed(comm, t, sc, steps, reps=3):
-    """min over `reps` runs of ms per step (the in-process transport creates
+def timed(comm, t, sc, steps, reps=5):
+    """ms per step of `reps` runs, sorted (the in-process transport creates
     and retires HIP events per message: occasional host stalls that RCCL
-    does not have)"""
-    return min(_timed(comm, t, sc, steps) for _ in range(reps))
+    does not have, so the min is the estimate)"""
+    return sorted(_timed(comm, t, sc, steps) for _ in range(reps))
 
 
 def _timed(comm, t, sc, steps):
@@ -60,20 +60,23 @@ def main():
         stencil.set_fusion(k)
         steps = 10 * max(k, 2)
         os.environ.pop("SMI_LOOPBACK", None)
-        alone = timed(comm, t, sc, steps)
-        for rounds in (2, 3, 4, 6):
+        alone = timed(comm, t, sc, steps)[0]
+        noxchg = os.environ.get("SMI_LOOPBACK_NOXCHG")
+        for rounds in [int(r) for r in os.environ.get("REHEARSAL_ROUNDS", "1,2,3,4,6").split(",")]:
             os.environ["SMI_ROUNDS_MULTI"] = str(rounds)
             for ov in (1, 0):
                 stencil.set_tuning(overlap=ov)
                 os.environ["SMI_LOOPBACK"] = "1"
-                loop = timed(comm, t, sc, steps)
+                runs = timed(comm, t, sc, steps)
+                loop = runs[0]
                 ring = profiling.read(profiling.EDGE)
                 sweep = profiling.read(profiling.SWEEPK if k >= 4 else profiling.SWEEP)
                 os.environ.pop("SMI_LOOPBACK", None)
-                print(json.dumps({"K": k, "rounds": rounds, "overlap": ov, "tile": n,
+                print(json.dumps({"K": k, "rounds": rounds, "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
                                   "ms_per_step_alone": round(alone, 5),
                                   "ms_per_step_interior_rank": round(loop, 5),
                                   "efficiency": round(alone / loop, 4),
+                                  "runs_ms_per_step": [round(r, 5) for r in runs],
                                   "ring_avg_ms": round(ring[0] / max(ring[1], 1), 5),
                                   "interior_avg_ms": round(sweep[0] / max(sweep[1], 1), 5)}), flush=True)
     stencil.set_tuning(overlap=1)
