@@ -25,6 +25,7 @@
 // [col_lo,col_hi) of the tile from input cells within K of it, so it is the
 // single-tile sweep (whole tile) and, in multi-rank runs, the interior sweep
 // that stays K cells clear of every halo-facing side.
+#include <cstdlib>
 #include <type_traits>
 
 #include "stencil_common.h"
@@ -56,30 +57,50 @@ __device__ __forceinline__ void static_for(F &&f) {
     static_for_from<0, N>(f);
 }
 
+// How a wave treats the global edge rows (stencil_smi.cl:143-151: rows 0 and
+// X-1 are copied unchanged every step).
+//   ROW_NONE  the wave's cone never reaches an edge row: no selects at all.
+//   ROW_TOP   the wave's first output row is row 0 (walk downwards).  Row 0
+//             of level l is produced at input t = K + l <= 2K, i.e. only in
+//             the compile-time prologue, so the copy is a handful of
+//             constant-index register moves there -- nothing in the loop.
+//   ROW_BOT   the wave's last output row is row X-1: the wave walks UPWARDS
+//             (N and S swap roles in the loads, never in the arithmetic
+//             order), so row X-1 is again its prologue row t - l = K.
+//   ROW_FULL  anything else that touches an edge row (blocks spanning both
+//             edges, tiny row blocks from a tuning override): per-cell
+//             row selects as before.
+// Column edges add one per-lane select per level step: CE bit 0 for the
+// strip holding column 0, bit 1 for the one holding column Y-1 (both only
+// when one window spans the whole tile); every other wave runs the plain
+// 12-instruction step.
+enum { ROW_NONE = 0, ROW_TOP = 1, ROW_BOT = 2, ROW_FULL = 3 };
+
 template <int K, int U, bool NT>
 struct SweepK {
     static_assert(K % 4 == 0 && K >= 4 && K <= 12, "K must be a multiple of 4 (float4 lanes)");
     static_assert(U % 3 == 0, "batch must be a multiple of the 3-slot ring");
-    static constexpr int LL = K / 4;  // lanes per side that never store
-    static constexpr int PRO = 2 * K; // prologue input rows
+    static constexpr int LL = K / 4;      // lanes per side that never store
+    static constexpr int PRO = 2 * K + 1; // prologue input rows (the last one stores the first output row)
 
     const float *__restrict__ in;
     float *__restrict__ out;
     int rows, cols;
     int o0, o1;       // output rows of this wave
-    int r_begin;      // first input row (o0 - K)
+    int r_begin;      // input row of t = 0 (o0 - K walking down, o1 - 1 + K walking up)
     int cl, cb;       // clamped load column / first column of this lane
     int voff;         // store byte offset in the row (out of range: no store)
     int row_bytes;
     bool st, copyL, copyR, gT, gB;
     float4 W[K][3];   // level 0..K-1, slot = input row index mod 3
 
+    template <bool REV>
     __device__ __forceinline__ float4 ld(int t) const {
-        const int r = min(max(r_begin + t, 0), rows - 1);
+        const int r = min(max(REV ? r_begin - t : r_begin + t, 0), rows - 1);
         return *reinterpret_cast<const float4 *>(in + (size_t)r * cols + cl);
     }
 
-    template <bool EDGE>
+    template <int ROW, int CE>
     __device__ __forceinline__ float4 step(int i, const float4 &n, const float4 &c, const float4 &s) const {
         const float w = shr1_any(c.w);
         const float e = shl1_any(c.x);
@@ -98,39 +119,55 @@ struct SweepK {
         o.y = o01.y;
         o.z = o23.x;
         o.w = o23.y;
-        if constexpr (EDGE) {
+        if constexpr (ROW == ROW_FULL) {
             const bool rcopy = (i == 0 && gT) || (i == rows - 1 && gB);
             o.x = (rcopy || copyL) ? c.x : o.x;
             o.y = rcopy ? c.y : o.y;
             o.z = rcopy ? c.z : o.z;
             o.w = (rcopy || copyR) ? c.w : o.w;
+        } else {
+            if constexpr (CE & 1) o.x = copyL ? c.x : o.x;
+            if constexpr (CE & 2) o.w = copyR ? c.w : o.w;
         }
         return o;
     }
 
-    // Input row t (index from r_begin) arrives with value x; PH = t mod 3.
-    template <bool EDGE, int PH>
+    // level l (1..K) at input t from the level l-1 rows of inputs t-2, t-1, t
+    // (slots PH+1, PH+2, PH mod 3).  Walking down, input t-2 is the upper
+    // row (N) and input t the lower (S); walking up they swap.
+    template <int ROW, int CE, int PH>
+    __device__ __forceinline__ float4 level(int l, int t, const float4 (&P)[3]) const {
+        if constexpr (ROW == ROW_BOT)
+            return step<ROW, CE>(r_begin - (t - l), P[PH], P[(PH + 2) % 3], P[(PH + 1) % 3]);
+        else
+            return step<ROW, CE>(r_begin + t - l, P[(PH + 1) % 3], P[(PH + 2) % 3], P[PH]);
+    }
+
+    // Input row t arrives with value x; PH = t mod 3.
+    template <int ROW, int CE, int PH>
     __device__ __forceinline__ void advance(int t, const float4 &x) {
         W[0][PH] = x;
         float4 v;
         static_for<K>([&](auto L) {
             constexpr int l = L + 1;
-            // level l-1 rows produced at inputs t-2, t-1, t live in slots PH+1, PH+2, PH (mod 3)
-            v = step<EDGE>(r_begin + t - l, W[l - 1][(PH + 1) % 3], W[l - 1][(PH + 2) % 3], W[l - 1][PH]);
+            v = level<ROW, CE, PH>(l, t, W[l - 1]);
             if constexpr (l < K) W[l][PH] = v;
         });
-        const int j = o0 + (t - PRO);  // level-K row produced by input t
-        store_row(j, v);
+        store_row<ROW == ROW_BOT>(t, v);
     }
 
-    // Branch-free predicated store: a buffer store through a per-row
-    // descriptor whose record count is the row's bytes (0 for rows past o1);
-    // lanes that must not store carry an offset beyond it and the hardware
-    // range check drops them.  No branch splits the unrolled rows, so the
-    // scheduler interleaves their dependency chains.
-    __device__ __forceinline__ void store_row(int j, const float4 &v) const {
-        const int jj = __builtin_amdgcn_readfirstlane(min(j, rows - 1));
-        const int nrec = __builtin_amdgcn_readfirstlane(j < o1 ? row_bytes : 0);
+    // Branch-free predicated store of the level-K row produced by input t:
+    // a buffer store through a per-row descriptor whose record count is the
+    // row's bytes (0 for rows outside [o0, o1)); lanes that must not store
+    // carry an offset beyond it and the hardware range check drops them.  No
+    // branch splits the unrolled rows, so the scheduler interleaves their
+    // dependency chains.
+    template <bool REV>
+    __device__ __forceinline__ void store_row(int t, const float4 &v) const {
+        const int j = REV ? o1 - 1 - (t - 2 * K) : o0 + (t - 2 * K);
+        const bool in_block = REV ? j >= o0 : j < o1;
+        const int jj = __builtin_amdgcn_readfirstlane(min(max(j, 0), rows - 1));
+        const int nrec = __builtin_amdgcn_readfirstlane(in_block ? row_bytes : 0);
         __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(out + (size_t)jj * cols, (short)0, nrec, 0x00020000);
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -139,44 +176,54 @@ struct SweepK {
         __builtin_amdgcn_raw_buffer_store_b128(d, rs, voff, 0, NT ? 2 : 0);
     }
 
-    template <bool EDGE>
+    template <int ROW, int CE>
     __device__ __forceinline__ void run() {
-        // prologue: input rows 0 .. 2K-1, compile-time indices
+        constexpr bool REV = ROW == ROW_BOT;
+        // prologue: input rows 0 .. 2K, compile-time indices; level l starts
+        // at input 2l (the first row it must produce)
         static_for<PRO>([&](auto T) {
             constexpr int t = T;
-            const float4 x = ld(t);
-            W[0][t % 3] = x;
+            W[0][t % 3] = ld<REV>(t);
+            float4 v;
             static_for<K>([&](auto L) {
                 constexpr int l = L + 1;
                 if constexpr (t >= 2 * l) {
-                    const float4 v = step<EDGE>(r_begin + t - l, W[l - 1][(t + 1) % 3], W[l - 1][(t + 2) % 3],
-                                                W[l - 1][t % 3]);
+                    v = level<ROW, CE, t % 3>(l, t, W[l - 1]);
+                    // the edge row (0 walking down, X-1 walking up) is input t - l == K
+                    if constexpr ((ROW == ROW_TOP || ROW == ROW_BOT) && t - l == K) v = W[l - 1][(t + 2) % 3];
                     if constexpr (l < K) W[l][t % 3] = v;
                 }
             });
+            if constexpr (t == 2 * K) store_row<REV>(t, v);
         });
         // steady state: 2U input rows per iteration, loads one batch ahead
-        const int n_in = (o1 - o0) + PRO;
+        const int n_in = (o1 - o0) + 2 * K;
         float4 A[U], B[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) A[u] = ld(PRO + u);
+        for (int u = 0; u < U; ++u) A[u] = ld<REV>(PRO + u);
         for (int t = PRO; t < n_in; t += 2 * U) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) B[u] = ld(t + U + u);
+            for (int u = 0; u < U; ++u) B[u] = ld<REV>(t + U + u);
             static_for<U>([&](auto V) {
                 constexpr int ph = (PRO + V) % 3;
-                advance<EDGE, ph>(t + V, A[V]);
+                advance<ROW, CE, ph>(t + V, A[V]);
             });
             if (t + U >= n_in) break;  // uniform
 #pragma unroll
-            for (int u = 0; u < U; ++u) A[u] = ld(t + 2 * U + u);
+            for (int u = 0; u < U; ++u) A[u] = ld<REV>(t + 2 * U + u);
             static_for<U>([&](auto V) {
                 constexpr int ph = (PRO + U + V) % 3;
-                advance<EDGE, ph>(t + U + V, B[V]);
+                advance<ROW, CE, ph>(t + U + V, B[V]);
             });
         }
     }
 };
+
+#ifdef SMI_LOOPBACK_REHEARSAL
+// rehearsal build only (timing experiments): 0 = normal, 1 = every wave runs
+// the global-edge variant, 2 = none does (results then wrong at the edges)
+__device__ int g_edge_force;
+#endif
 
 template <int K, int U, bool NT>
 __global__ __launch_bounds__(256) void sweepk_kernel(const float *__restrict__ in, float *__restrict__ out,
@@ -194,9 +241,10 @@ __global__ __launch_bounds__(256) void sweepk_kernel(const float *__restrict__ i
     w.out = out;
     w.rows = a.rows;
     w.cols = a.cols;
-    w.o0 = a.row_lo + rb * ht;
-    w.o1 = min(w.o0 + ht, a.row_hi);
-    w.r_begin = w.o0 - K;
+    // balanced row blocks: every block of a tall rectangle has >= ht/2 rows
+    const int out_rows = a.row_hi - a.row_lo;
+    w.o0 = a.row_lo + (int)((long)rb * out_rows / nrb);
+    w.o1 = a.row_lo + (int)((long)(rb + 1) * out_rows / nrb);
     const int cs = a.col_lo + strip * SW;
     w.cb = cs - K + 4 * lane;
     w.cl = min(max(w.cb, 0), a.cols - 4);
@@ -208,12 +256,36 @@ __global__ __launch_bounds__(256) void sweepk_kernel(const float *__restrict__ i
     w.gT = a.gT;
     w.gB = a.gB;
     // rows any level touches: [o0 - 2K, o1 + K + 5); columns: [cs - K, cs - K + 256)
-    const bool edge = (a.gT && w.o0 - 2 * K <= 0) || (a.gB && w.o1 + K + 6 >= a.rows) ||
-                      (a.gL && cs - K <= 0) || (a.gR && cs - K + 256 >= a.cols);
-    if (edge)
-        w.template run<true>();
-    else
-        w.template run<false>();
+    const bool touchT = a.gT && w.o0 - 2 * K <= 0;
+    const bool touchB = a.gB && w.o1 + K + 6 >= a.rows;
+    int ce = ((a.gL && cs - K <= 0) ? 1 : 0) | ((a.gR && cs - K + 256 >= a.cols) ? 2 : 0);
+    int row = ROW_NONE;
+    if (touchT && !touchB && w.o0 == 0)
+        row = ROW_TOP;
+    else if (touchB && !touchT && w.o1 == a.rows)
+        row = ROW_BOT;
+    else if (touchT || touchB)
+        row = ROW_FULL;
+#ifdef SMI_LOOPBACK_REHEARSAL
+    if (g_edge_force == 1) row = ROW_FULL;
+    if (g_edge_force == 2) row = ROW_NONE, ce = 0;
+#endif
+    w.r_begin = row == ROW_BOT ? w.o1 - 1 + K : w.o0 - K;
+    switch (row * 4 + ce) {
+    case 0: w.template run<ROW_NONE, 0>(); break;
+    case 1: w.template run<ROW_NONE, 1>(); break;
+    case 2: w.template run<ROW_NONE, 2>(); break;
+    case 3: w.template run<ROW_NONE, 3>(); break;
+    case 4: w.template run<ROW_TOP, 0>(); break;
+    case 5: w.template run<ROW_TOP, 1>(); break;
+    case 6: w.template run<ROW_TOP, 2>(); break;
+    case 7: w.template run<ROW_TOP, 3>(); break;
+    case 8: w.template run<ROW_BOT, 0>(); break;
+    case 9: w.template run<ROW_BOT, 1>(); break;
+    case 10: w.template run<ROW_BOT, 2>(); break;
+    case 11: w.template run<ROW_BOT, 3>(); break;
+    default: w.template run<ROW_FULL, 3>(); break;
+    }
 }
 
 template <int K, int U>
@@ -275,6 +347,17 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
     const int nrb = (out_rows + ht - 1) / ht;
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
+#ifdef SMI_LOOPBACK_REHEARSAL
+    {
+        static int cur = 0;
+        const char *e = getenv("SMI_EDGE_FORCE");
+        const int want = e ? atoi(e) : 0;
+        if (want != cur) {
+            SMI_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_edge_force), &want, sizeof(int)));
+            cur = want;
+        }
+    }
+#endif
     int tok = -1;
     if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok));
     const bool nt = g_tune.nt;
