@@ -225,8 +225,11 @@ def aux_collectives(comm, world: int, rank: int, stream, barrier) -> list:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=120)
-    ap.add_argument("--warmup", type=int, default=10)
+    # ~25 ms of untimed warm-up: the GPU clock needs >10 ms of load to reach
+    # its steady state (120 steps after 10 warm-up steps measured ~11 % low,
+    # profiles/r01f/bench_warmup_sweep.log); 2400 timed steps = 200 K-step passes
+    ap.add_argument("--steps", type=int, default=2400)
+    ap.add_argument("--warmup", type=int, default=2400)
     ap.add_argument("--tile", type=int, default=TILE)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aux", action="store_true",

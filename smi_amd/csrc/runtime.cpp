@@ -100,7 +100,10 @@ static int prof_get_event(hipEvent_t *e) {
         g_prof_pool.pop_back();
         return SMI_SUCCESS;
     }
-    SMI_HIP_CHECK(hipEventCreate(e));
+    // timing markers only: no system-scope release/acquire (a default event
+    // fences at system scope, which cost ~1 us per marker between
+    // back-to-back sweep launches)
+    SMI_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableSystemFence));
     return SMI_SUCCESS;
 }
 
