@@ -15,11 +15,12 @@
 // slot = (input row index) mod 3; the loop body covers 6 input rows (two
 // batches of 3, each batch's loads issued one batch ahead), so every slot
 // index is a compile-time constant and no value is ever moved between
-// registers.  The first 2K input rows of a row block only prime the
-// pipeline; that prologue is unrolled with compile-time row indices and
+// registers (a third register batch, loads two batches ahead, measured no
+// faster: profiles/r01f).  The first 2K+1 input rows of a row block prime
+// the pipeline; that prologue is unrolled with compile-time row indices and
 // evaluates level l only from input row 2l on (the rows it must produce).
-// Waves whose rows or columns touch a global edge run a variant with the
-// copy rules; all others run without any per-cell selects.
+// Global-edge copy rules cost nothing in the loop (ROW_* below); only the
+// strips holding column 0 or Y-1 add a per-lane select.
 //
 // The kernel computes an arbitrary output rectangle [row_lo,row_hi) x
 // [col_lo,col_hi) of the tile from input cells within K of it, so it is the
