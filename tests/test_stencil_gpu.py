@@ -307,3 +307,46 @@ def test_deep_decomposed_small_tiles(gpu, oracle_mod, k):
     # config 1 (256^2, 2x2, 32 steps) through the deep path
     g = oracle_mod.init_edges(256, 256)
     assert np.array_equal(bits(_run_fused(g, 32, 2, 2, k=k)), bits(oracle_mod.stencil_decomposed(g, 32, 2, 2)))
+
+
+# ------------------------------------------ special values through every path --
+def _special_grid(X, Y, seed):
+    """Uniform grid salted with the values IEEE fp32 treats specially: signed
+    zeros, subnormals, the largest finite values, infinities and NaN."""
+    rng = np.random.default_rng(seed)
+    g = (rng.random((X, Y), dtype=np.float32) * 2 - 1).astype(np.float32)
+    salt = np.array([0.0, -0.0, 1e-40, -1e-40, 1.4e-45, 1.17549435e-38, 3.4e38, -3.4e38],
+                    dtype=np.float32)
+    idx = rng.integers(0, X * Y, size=X * Y // 7)
+    g.reshape(-1)[idx] = salt[rng.integers(0, len(salt), size=len(idx))]
+    # a patch of tiny values whose averages go subnormal and back
+    g[X // 3:X // 3 + 5, Y // 4:Y // 4 + 40] = np.float32(3e-38)
+    # a few isolated non-finite cells (they spread one cell per step), one on
+    # a global edge, one next to a tile boundary of a 2x2 decomposition
+    for (r, c), v in zip([(5, 7), (X - 1, Y // 3), (X // 2 - 1, Y // 2), (X - 9, Y - 3)],
+                         [np.nan, np.inf, -np.inf, np.nan]):
+        g[r, c] = v
+    return g
+
+
+def _same(a, b):
+    """Bit-identical, except that any NaN matches any NaN (payload propagation
+    is not part of the reference's contract)."""
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(bits(np.where(na, 0, a)), bits(np.where(nb, 0, b)))
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 12])
+@pytest.mark.parametrize("pxpy", [(1, 1), (2, 2)])
+def test_special_values_bit_exact(gpu, oracle_mod, k, pxpy):
+    PX, PY = pxpy
+    g = _special_grid(96 * PX, 264 * PY, seed=k + 7 * PX)
+    for T in (1, k + 1, 2 * k + 3):
+        got = _run_fused(g, T, PX, PY, k=k)
+        assert _same(got, oracle_mod.stencil(g, T)), (k, pxpy, T)
+
+
+def test_special_values_single_steps(gpu, oracle_mod):
+    g = _special_grid(70, 132, seed=3)
+    assert _same(run_steps(g, 5), oracle_mod.stencil(g, 5))
