@@ -29,7 +29,8 @@ The JSON line also carries:
   aux           -- measured after the timed stencil region (skip: --no-aux):
                    gesummv 32768^2 row-sharded over the N GPUs (BASELINE
                    config 5) and, for N>1, SMI_Reduce int32/fp32 and SMI_Bcast
-                   at 4 KiB-256 MiB (config 4) with algbw vs the xGMI bound;
+                   at 4 KiB-256 MiB (config 4) with algbw vs the xGMI bound,
+                   and the p2p bandwidth/latency microbenchmarks on one link;
                    bounded by a watchdog so the stencil line always prints
 """
 from __future__ import annotations
@@ -156,6 +157,17 @@ def _timed(fn, iters: int, barrier, world: int) -> float:
     return dt
 
 
+def _all_ok(ok: bool, world: int) -> bool:
+    """A check made on one rank, agreed by every rank (rank 0 prints)."""
+    if world == 1:
+        return ok
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0])
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
 def aux_gesummv(comm, world: int, rank: int, stream, barrier) -> dict:
     """BASELINE config 5: y = alpha*A*x + beta*B*x, 32768^2 fp32, rows sharded
     over the ranks (strong scaling), y chunks gathered on rank 0
@@ -182,6 +194,60 @@ def aux_gesummv(comm, world: int, rank: int, stream, barrier) -> dict:
     return {"workload": f"gesummv {n}x{m} fp32, {world}-way row shard, y gathered on rank 0",
             "ms": round(dt * 1e3, 4), "GBs": round(gbs, 1),
             "hbm_frac": round(gbs / (HBM_PEAK_GBS * world), 4)}
+
+
+def aux_p2p(comm, world: int, rank: int, stream, barrier) -> dict:
+    """p2p microbenchmarks (microbenchmarks/kernels/bandwidth_*.cl,
+    latency_*.cl) over one xGMI link, rank 0 -> rank 1 through smi_send /
+    smi_recv: bandwidth at 4 KiB - 256 MiB of doubles 0.1f + i (checked on
+    rank 1), and the one-int ping-pong latency (round trip / 2)."""
+    import torch
+    from smi_amd import collectives
+    bw = []
+    start = float(np.float32(0.1))
+    for nbytes in COLL_BYTES:
+        n = nbytes // 8
+        if rank == 0:
+            buf = start + torch.arange(n, dtype=torch.float64, device="cuda")
+        else:
+            buf = torch.zeros(n, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
+
+        def call():
+            if rank == 0:
+                collectives.send(comm, buf, 1, stream=stream)
+            elif rank == 1:
+                collectives.recv(comm, buf, 0, stream=stream)
+
+        with torch.cuda.stream(stream):
+            t = _timed(call, 20 if nbytes <= (1 << 20) else 5, barrier, world)
+        ok = True
+        if rank == 1:
+            ok = bool((buf == start + torch.arange(n, dtype=torch.float64, device="cuda")).all().item())
+        gbs = nbytes / t / 1e9
+        row = {"bytes": nbytes, "us": round(t * 1e6, 1), "GBs": round(gbs, 2),
+               "link_frac": round(gbs / XGMI_LINK_GBS, 4)}
+        if not _all_ok(ok, world):
+            row["error"] = "KAT mismatch on rank 1"
+        bw.append(row)
+        del buf
+    v = torch.zeros(1, dtype=torch.int32, device="cuda")
+    trips = 100
+
+    def pingpong():
+        for _ in range(trips):
+            if rank == 0:
+                collectives.send(comm, v, 1, stream=stream)
+                collectives.recv(comm, v, 1, stream=stream)
+            elif rank == 1:
+                collectives.recv(comm, v, 0, stream=stream)
+                v.add_(1)
+                collectives.send(comm, v, 0, stream=stream)
+
+    with torch.cuda.stream(stream):
+        t = _timed(pingpong, 1, barrier, world)
+    return {"pair": [0, 1], "bandwidth": bw, "latency_us": round(t / (2 * trips) * 1e6, 2),
+            "note": "latency = ping-pong round trip / 2 of one int32, stream-ordered smi_send/smi_recv"}
 
 
 def aux_collectives(comm, world: int, rank: int, stream, barrier) -> list:
@@ -216,8 +282,8 @@ def aux_collectives(comm, world: int, rank: int, stream, barrier) -> list:
             gbs = nbytes / t / 1e9
             out.append({"op": op, "bytes": nbytes, "us": round(t * 1e6, 1), "algbw_GBs": round(gbs, 2),
                         "xgmi_bound_GBs": bound, "xgmi_frac": round(gbs / bound, 4)})
-        if not ok:
-            out.append({"op": "reduce_i32_add", "bytes": nbytes, "error": "KAT mismatch"})
+        if not _all_ok(ok, world):
+            out.append({"op": "reduce_i32_add", "bytes": nbytes, "error": "KAT mismatch on the root"})
         del snd_i, snd_f, rcv, rcv_i, buf
     return out
 
@@ -401,6 +467,7 @@ def main() -> None:
             aux["gesummv"] = aux_gesummv(comm, world, rank, stream, barrier)
             if world > 1:
                 aux["collectives"] = aux_collectives(comm, world, rank, stream, barrier)
+                aux["p2p"] = aux_p2p(comm, world, rank, stream, barrier)
         except Exception as e:  # report, never lose the stencil line
             aux["error"] = f"{type(e).__name__}: {e}"
         out["aux"] = aux

@@ -21,6 +21,12 @@ SMI_Channel SMI_Open_receive_channel_ad(int count, SMI_Datatype data_type, int s
                                         SMI_Comm comm, int asynch_degree);
 void SMI_Pop(SMI_Channel *chan, void *data);
 
+/* Bulk, device-buffer form of a receive channel: `count` elements from
+ * `source` into `buf` (device memory), enqueued on `stream`.  Replaces a
+ * SMI_Open_receive_channel + count x SMI_Pop loop (bandwidth_1.cl:12-44). */
+int smi_recv(SMI_Comm comm, void *buf, size_t count, SMI_Datatype data_type, int source, int port,
+             SMI_Stream stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,6 +27,14 @@ SMI_Channel SMI_Open_send_channel_ad(int count, SMI_Datatype data_type, int dest
 void SMI_Push_flush(SMI_Channel *chan, void *data, int immediate);
 void SMI_Push(SMI_Channel *chan, void *data);
 
+/* Bulk, device-buffer form of a send channel: `count` elements of `buf`
+ * (device memory) to `destination`, enqueued on `stream`.  Replaces a
+ * SMI_Open_send_channel + count x SMI_Push loop (bandwidth_0.cl:13-35).
+ * Pairs with smi_recv on the destination; messages between two ranks are
+ * matched in issue order (the port is informational). */
+int smi_send(SMI_Comm comm, const void *buf, size_t count, SMI_Datatype data_type, int destination,
+             int port, SMI_Stream stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,6 +68,8 @@ SIGNATURES = {
     "smi_type_size": (SZ, [I]),
     "smi_scatter": (I, [SMI_Comm, P, P, SZ, I, I, I, P]),
     "smi_gather": (I, [SMI_Comm, P, P, SZ, I, I, I, P]),
+    "smi_send": (I, [SMI_Comm, P, SZ, I, I, I, P]),
+    "smi_recv": (I, [SMI_Comm, P, SZ, I, I, I, P]),
     "smi_gemv_rows": (I, [P, P, P, P, I, I, I, F, F, P]),
     "smi_gesummv": (I, [SMI_Comm, P, P, P, P, I, I, F, F, I, P]),
     "smi_kmeans_assign": (I, [P, I, I, P, I, I, P, P]),

@@ -72,3 +72,16 @@ def gather(comm: Comm, send: torch.Tensor, recv: torch.Tensor | None, root: int 
     root's `recv`."""
     _lib.call("smi_gather", comm.handle, send.data_ptr(), None if recv is None else recv.data_ptr(),
               send.numel(), _smi_type(send), root, port, _lib.stream_handle(stream))
+
+
+def send(comm: Comm, buf: torch.Tensor, dest: int, port: int = 0, stream=None) -> None:
+    """Bulk send channel: every element of device tensor `buf` to `dest`
+    (smi_send; a SMI_Open_send_channel + SMI_Push loop in the reference)."""
+    _lib.call("smi_send", comm.handle, buf.data_ptr(), buf.numel(), _smi_type(buf), dest, port,
+              _lib.stream_handle(stream))
+
+
+def recv(comm: Comm, buf: torch.Tensor, source: int, port: int = 0, stream=None) -> None:
+    """Bulk receive channel into device tensor `buf` from `source` (smi_recv)."""
+    _lib.call("smi_recv", comm.handle, buf.data_ptr(), buf.numel(), _smi_type(buf), source, port,
+              _lib.stream_handle(stream))

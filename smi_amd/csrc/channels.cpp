@@ -545,6 +545,24 @@ int smi_scatter(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count,
     return tp->end();
 }
 
+// Bulk point-to-point on device buffers, stream-ordered: the GPU-native form
+// of a transient channel that carries `count` elements from one rank to
+// another (push.h / pop.h; the reference's bandwidth microbenchmark streams
+// N elements through SMI_Push/SMI_Pop, microbenchmarks/kernels/
+// bandwidth_0.cl:13-35, bandwidth_1.cl:12-44).  One transport message (an
+// RCCL send/recv over xGMI, or a device copy in-process).  Messages between
+// a pair of ranks are matched in the order they are issued, whatever their
+// port (RCCL keeps one FIFO per pair), so a port here is informational.
+static int p2p_check(Comm *c, size_t esz, int peer) {
+    if (esz == 0) {
+        set_error("unsupported data type");
+        return SMI_ERR_UNSUPPORTED;
+    }
+    SMI_ARG_CHECK(peer >= 0 && peer < c->size, "peer rank out of range");
+    SMI_ARG_CHECK(peer != c->rank, "point-to-point to self");
+    return SMI_SUCCESS;
+}
+
 int smi_gather(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count, SMI_Datatype type, int root,
                int port, SMI_Stream stream) {
     (void)port;
@@ -575,6 +593,42 @@ int smi_gather(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count, 
     } else {
         SMI_TRY(tp->send(sendbuf, bytes, root));
     }
+    return tp->end();
+}
+
+
+int smi_send(SMI_Comm comm, const void *buf, size_t count, SMI_Datatype type, int destination, int port,
+             SMI_Stream stream) {
+    (void)port;
+    Comm *c = lookup_comm(comm);
+    if (!c) {
+        set_error("unknown communicator");
+        return SMI_ERR_BAD_COMM;
+    }
+    const size_t esz = type_size(type);
+    SMI_TRY(p2p_check(c, esz, destination));
+    if (count == 0) return SMI_SUCCESS;
+    SMI_ARG_CHECK(buf, "NULL buffer");
+    Transport *tp = c->transport.get();
+    SMI_TRY(tp->begin((hipStream_t)stream));
+    SMI_TRY(tp->send(buf, count * esz, destination));
+    return tp->end();
+}
+
+int smi_recv(SMI_Comm comm, void *buf, size_t count, SMI_Datatype type, int source, int port, SMI_Stream stream) {
+    (void)port;
+    Comm *c = lookup_comm(comm);
+    if (!c) {
+        set_error("unknown communicator");
+        return SMI_ERR_BAD_COMM;
+    }
+    const size_t esz = type_size(type);
+    SMI_TRY(p2p_check(c, esz, source));
+    if (count == 0) return SMI_SUCCESS;
+    SMI_ARG_CHECK(buf, "NULL buffer");
+    Transport *tp = c->transport.get();
+    SMI_TRY(tp->begin((hipStream_t)stream));
+    SMI_TRY(tp->recv(buf, count * esz, source));
     return tp->end();
 }
 

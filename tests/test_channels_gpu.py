@@ -278,3 +278,76 @@ def test_balanced_routing_broadcast_kat(gpu, N, root):
         return ok
 
     assert all(group(8, fn))
+
+
+@pytest.mark.parametrize("N", [1, 1000, 1 << 20])
+@pytest.mark.parametrize("dest", [1, 4, 7])
+def test_bulk_p2p_bandwidth_kat(gpu, N, dest):
+    """microbenchmarks/kernels/bandwidth_0.cl / bandwidth_1.cl: rank 0 streams
+    N doubles 0.1f + i to `dest` on two ports; the receiver checks every one."""
+    from smi_amd import collectives
+    start = np.float64(np.float32(0.1))
+    want = start + np.arange(N, dtype=np.float64)
+
+    def fn(comm):
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            ok = True
+            for port in (0, 1):
+                if comm.rank == 0:
+                    collectives.send(comm, torch.from_numpy(want).cuda(), dest, port, stream=s)
+                elif comm.rank == dest:
+                    got = torch.zeros(N, dtype=torch.float64, device="cuda")
+                    collectives.recv(comm, got, 0, port, stream=s)
+                    s.synchronize()
+                    ok &= np.array_equal(got.cpu().numpy(), want)
+            s.synchronize()
+            return ok
+
+    assert all(group(8, fn))
+
+
+def test_bulk_p2p_latency_pingpong_and_order(gpu):
+    """microbenchmarks/kernels/latency_0.cl / latency_1.cl: one int bounces
+    between ranks 0 and 1, rank 1 increments it; then three messages of
+    different sizes between one pair arrive in issue order."""
+    from smi_amd import collectives
+
+    def fn(comm):
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            v = torch.zeros(1, dtype=torch.int32, device="cuda")
+            for _ in range(50):
+                if comm.rank == 0:
+                    collectives.send(comm, v, 1, stream=s)
+                    collectives.recv(comm, v, 1, stream=s)
+                else:
+                    collectives.recv(comm, v, 0, stream=s)
+                    v += 1
+                    collectives.send(comm, v, 0, stream=s)
+            sizes = (3, 1 << 16, 17)
+            if comm.rank == 0:
+                for k, n in enumerate(sizes):
+                    collectives.send(comm, torch.full((n,), k + 1, dtype=torch.int16, device="cuda"), 1,
+                                     stream=s)
+                s.synchronize()
+                return int(v.item()) == 50
+            got = [torch.zeros(n, dtype=torch.int16, device="cuda") for n in sizes]
+            for k, g in enumerate(got):
+                collectives.recv(comm, g, 0, stream=s)
+            s.synchronize()
+            return int(v.item()) == 50 and all(bool((g == k + 1).all()) for k, g in enumerate(got))
+
+    assert all(group(2, fn))
+
+
+def test_bulk_p2p_errors(gpu):
+    from smi_amd import LocalGroup, collectives
+    from smi_amd._lib import SMIError
+    comm = LocalGroup(1).comm(0)
+    buf = torch.zeros(4, device="cuda")
+    with pytest.raises(SMIError):
+        collectives.send(comm, buf, 0)      # to self
+    with pytest.raises(SMIError):
+        collectives.recv(comm, buf, 3)      # peer out of range
+    comm.finalize()

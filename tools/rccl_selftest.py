@@ -57,6 +57,19 @@ def main():
         good = np.array_equal(buf.cpu().numpy(), data)
         print(f"[{rank}] bcast: {'OK' if good else 'MISMATCH'}", flush=True)
         ok &= good
+        # bulk p2p (smi_send / smi_recv): rank 0 -> last rank, bandwidth_*.cl KAT
+        n = (1 << 20) + 3
+        want = np.float64(np.float32(0.1)) + np.arange(n, dtype=np.float64)
+        if rank == 0:
+            collectives.send(comm, torch.from_numpy(want).cuda(), world - 1)
+        elif rank == world - 1:
+            got = torch.zeros(n, dtype=torch.float64, device="cuda")
+            collectives.recv(comm, got, 0)
+            s.synchronize()
+            good = np.array_equal(got.cpu().numpy(), want)
+            print(f"[{rank}] p2p send/recv: {'OK' if good else 'MISMATCH'}", flush=True)
+            ok &= good
+        s.synchronize()
         # decomposed stencil (1 x world, or 2 x world/2)
         PX, PY = (2, world // 2) if world % 2 == 0 and world >= 4 else (1, world)
         g = oracle.init_uniform(256 * PX, 256 * PY, seed=5)
