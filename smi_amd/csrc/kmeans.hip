@@ -16,7 +16,7 @@
 //   base_kernel      exclusive prefix over the clusters
 //   scatter_kernel   order-preserving compaction: list = the points of
 //                    cluster 0 in point order, then those of cluster 1, ...
-//   fold_kernel      one workgroup per (cluster, 64 dimensions): all waves
+//   fold_kernel      one workgroup per (cluster, 16 dimensions): all waves
 //                    gather the cluster's rows into an LDS tile, wave 0 adds
 //                    them in point order while the next tile is in flight
 //   smi_reduce / smi_bcast (collectives.hip), divide_kernel
@@ -37,7 +37,10 @@ constexpr int kPtsPerBlock = 256;  // assign / count / scatter
 constexpr int kMaxClusters = 256;
 constexpr int kQReg = 16;          // distance lanes held in registers
 constexpr int kFoldWaves = 8;
-constexpr int kRowsPerWave = 32;
+constexpr int kFoldDims = 16;                       // dimensions per workgroup (64-B row pieces)
+constexpr int kRowsPerLoad = 64 / kFoldDims;        // rows one wave-load covers
+constexpr int kLoadsPerWave = 32;
+constexpr int kRowsPerWave = kLoadsPerWave * kRowsPerLoad;
 constexpr int kFoldRows = kFoldWaves * kRowsPerWave;  // rows per LDS tile (64 KiB)
 
 // ComputeDistance (kmeans_smi.cl:54-85): per W-wide vector only the last
@@ -196,52 +199,77 @@ __global__ __launch_bounds__(kPtsPerBlock) void scatter_kernel(const int *__rest
 
 // ComputeMeans accumulation (kmeans_smi.cl:113-127): sums[k][d] = the fp32
 // chain over the points of cluster k in point order, from +0.  The chain is
-// serial, so the workgroup's job is to keep it fed: all waves gather the
-// next tile of rows (coalesced 256 B per row and wave) into registers while
-// wave 0 adds the current tile from LDS.
+// serial, so the workgroup's job is to keep it fed.  A CU fetches ~11 B/cycle,
+// so one workgroup per cluster would cap a chain at ~10 ns per point for 64
+// dims: each workgroup takes 16 dimensions (64-B row pieces, 4 rows per
+// wave-load) and all its waves gather rows two tiles ahead into registers and stage them into a double-buffered
+// LDS tile, while wave 0 adds the current tile in point order.  One barrier
+// per tile: tile t+1 goes into the buffer tile t-1 used, which every wave
+// finished with before the previous barrier.
 __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(const float *__restrict__ pts, int dims,
                                                               const int *__restrict__ list,
                                                               const int *__restrict__ counts,
                                                               const int *__restrict__ base,
                                                               float *__restrict__ sums) {
-    __shared__ float tile[kFoldRows][64];
+    __shared__ float tile[2][kFoldRows][kFoldDims];
     const int k = blockIdx.x;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int d = blockIdx.y * 64 + lane;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int sub = lane / kFoldDims;                 // row within a wave-load
+    const int d = blockIdx.y * kFoldDims + (lane % kFoldDims);
     const int dc = min(d, dims - 1);
     const int cnt = counts[k];
     const int *lst = list + base[k];
     const int ntiles = (cnt + kFoldRows - 1) / kFoldRows;
-    float v[kRowsPerWave];
-    auto gather = [&](int t) {
+    float va[kLoadsPerWave], vb[kLoadsPerWave];
+    auto gather = [&](float (&v)[kLoadsPerWave], int t) {
 #pragma unroll
-        for (int r = 0; r < kRowsPerWave; ++r) {
-            const int j = min(t * kFoldRows + w * kRowsPerWave + r, cnt - 1);
+        for (int r = 0; r < kLoadsPerWave; ++r) {
+            const int j = min(t * kFoldRows + w * kRowsPerWave + r * kRowsPerLoad + sub, cnt - 1);
             v[r] = pts[(size_t)lst[j] * dims + dc];
         }
     };
-    auto put = [&]() {
+    auto put = [&](const float (&v)[kLoadsPerWave], int t) {
 #pragma unroll
-        for (int r = 0; r < kRowsPerWave; ++r) tile[w * kRowsPerWave + r][lane] = v[r];
+        for (int r = 0; r < kLoadsPerWave; ++r)
+            tile[t & 1][w * kRowsPerWave + r * kRowsPerLoad + sub][lane % kFoldDims] = v[r];
     };
     float acc = 0.f;
-    if (ntiles > 0) {
-        gather(0);
-        put();
-        __syncthreads();
-        for (int t = 0; t < ntiles; ++t) {
-            if (t + 1 < ntiles) gather(t + 1);
-            if (w == 0) {
-                const int rows = min(kFoldRows, cnt - t * kFoldRows);
-#pragma unroll 8
-                for (int r = 0; r < rows; ++r) acc = __fadd_rn(acc, tile[r][lane]);
+    auto add = [&](int t) {
+        if (w == 0) {
+            const int rows = min(kFoldRows, cnt - t * kFoldRows);
+            const float(*tl)[kFoldDims] = tile[t & 1];
+            const int c = lane % kFoldDims;  // lanes >= kFoldDims repeat lane c's chain
+            // 16 LDS reads in flight ahead of the dependent adds (lgkmcnt holds 15)
+            int r = 0;
+            for (; r + 16 <= rows; r += 16) {
+                float x[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] = tl[r + i][c];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc = __fadd_rn(acc, x[i]);
             }
-            __syncthreads();
-            if (t + 1 < ntiles) put();
-            __syncthreads();
+            for (; r < rows; ++r) acc = __fadd_rn(acc, tl[r][c]);
+        }
+    };
+    // one pipeline step: tile t is in LDS, `cur` holds tile t+1, `nxt` gets t+2
+    auto step = [&](float (&cur)[kLoadsPerWave], float (&nxt)[kLoadsPerWave], int t) {
+        if (t + 2 < ntiles) gather(nxt, t + 2);
+        add(t);
+        if (t + 1 < ntiles) put(cur, t + 1);
+        __syncthreads();
+    };
+    if (ntiles > 0) {
+        gather(va, 0);
+        if (ntiles > 1) gather(vb, 1);
+        put(va, 0);
+        __syncthreads();
+        for (int t = 0; t < ntiles; t += 2) {
+            step(vb, va, t);
+            if (t + 1 < ntiles) step(va, vb, t + 1);
         }
     }
-    if (w == 0 && d < dims) sums[(size_t)k * dims + d] = acc;
+    if (w == 0 && lane < kFoldDims && d < dims) sums[(size_t)k * dims + d] = acc;
 }
 
 // centroid = sum / (float)count, IEEE division (kmeans_smi.cl:196-205)
@@ -320,7 +348,7 @@ static int launch_accumulate(const float *pts, int n, int dims, const int *idx, 
                            w.base, w.list);
     int tok = -1;
     if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_KMEANS_FOLD, s, &tok));
-    hipLaunchKernelGGL(fold_kernel, dim3(clusters, (dims + 63) / 64), dim3(64 * kFoldWaves), 0, s, pts, dims,
+    hipLaunchKernelGGL(fold_kernel, dim3(clusters, (dims + kFoldDims - 1) / kFoldDims), dim3(64 * kFoldWaves), 0, s, pts, dims,
                        w.list, counts, w.base, sums);
     SMI_HIP_CHECK(hipGetLastError());
     if (tok >= 0) SMI_TRY(prof_end(tok, s));
