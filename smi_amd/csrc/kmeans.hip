@@ -37,7 +37,7 @@ constexpr int kPtsPerBlock = 256;  // assign / count / scatter
 constexpr int kMaxClusters = 256;
 constexpr int kQReg = 16;          // distance lanes held in registers
 constexpr int kFoldWaves = 8;
-constexpr int kFoldDims = 16;                       // dimensions per workgroup (64-B row pieces)
+constexpr int kFoldDims = 8;                        // dimensions per workgroup (64-B row pieces)
 constexpr int kRowsPerLoad = 64 / kFoldDims;        // rows one wave-load covers
 constexpr int kLoadsPerWave = 32;
 constexpr int kRowsPerWave = kLoadsPerWave * kRowsPerLoad;
