@@ -37,7 +37,7 @@ constexpr int kPtsPerBlock = 256;  // assign / count / scatter
 constexpr int kMaxClusters = 256;
 constexpr int kQReg = 16;          // distance lanes held in registers
 constexpr int kFoldWaves = 8;
-constexpr int kFoldDims = 8;                        // dimensions per workgroup (64-B row pieces)
+constexpr int kFoldDims = 8;                        // dimensions per workgroup (32-B row pieces)
 constexpr int kRowsPerLoad = 64 / kFoldDims;        // rows one wave-load covers
 constexpr int kLoadsPerWave = 32;
 constexpr int kRowsPerWave = kLoadsPerWave * kRowsPerLoad;
@@ -211,7 +211,10 @@ __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(const float *__re
                                                               const int *__restrict__ counts,
                                                               const int *__restrict__ base,
                                                               float *__restrict__ sums) {
-    __shared__ float tile[2][kFoldRows][kFoldDims];
+    // transposed tile [dim][row]: a chain reads 4 rows per ds_read_b128; the
+    // +8 pad puts the 8 dims x 8 rows of one wave-store in 64 distinct banks
+    constexpr int TS = kFoldRows + 8;
+    __shared__ __attribute__((aligned(16))) float tile[2][kFoldDims][TS];
     const int k = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -232,24 +235,25 @@ __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(const float *__re
     auto put = [&](const float (&v)[kLoadsPerWave], int t) {
 #pragma unroll
         for (int r = 0; r < kLoadsPerWave; ++r)
-            tile[t & 1][w * kRowsPerWave + r * kRowsPerLoad + sub][lane % kFoldDims] = v[r];
+            tile[t & 1][lane % kFoldDims][w * kRowsPerWave + r * kRowsPerLoad + sub] = v[r];
     };
     float acc = 0.f;
     auto add = [&](int t) {
         if (w == 0) {
             const int rows = min(kFoldRows, cnt - t * kFoldRows);
-            const float(*tl)[kFoldDims] = tile[t & 1];
             const int c = lane % kFoldDims;  // lanes >= kFoldDims repeat lane c's chain
+            const float *tl = tile[t & 1][c];
             // 16 LDS reads in flight ahead of the dependent adds (lgkmcnt holds 15)
             int r = 0;
             for (; r + 16 <= rows; r += 16) {
-                float x[16];
+                float4 x4[4];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) x[i] = tl[r + i][c];
+                for (int i = 0; i < 4; ++i) x4[i] = *reinterpret_cast<const float4 *>(tl + r + 4 * i);
+                const float *x = reinterpret_cast<const float *>(x4);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) acc = __fadd_rn(acc, x[i]);
             }
-            for (; r < rows; ++r) acc = __fadd_rn(acc, tl[r][c]);
+            for (; r < rows; ++r) acc = __fadd_rn(acc, tl[r]);
         }
     };
     // one pipeline step: tile t is in LDS, `cur` holds tile t+1, `nxt` gets t+2
