@@ -41,6 +41,12 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+__device__ __forceinline__ float4 ld_stream(const float *p) {
+    using V4 = float __attribute__((ext_vector_type(4)));
+    const V4 v = __builtin_nontemporal_load(reinterpret_cast<const V4 *>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 constexpr int kGemvWaves = 4;
 constexpr int kSlabStride = 17;  // float4s per chunk in LDS (64 floats + 4 pad: conflict-free)
 
@@ -85,8 +91,8 @@ __global__ __launch_bounds__(64 * kGemvWaves) void gemv_rows_kernel(const float 
             const int ch = min(cbase + 4 * j + (lane >> 4), nchunks - 1);  // clamped: the tail
             const int e = ch * 64 + (lane & 15) * 4;                       // chunk's c is replaced
             const float4 xv = *reinterpret_cast<const float4 *>(x + e);
-            pa[j] = mul4(*reinterpret_cast<const float4 *>(a + e), xv);
-            if constexpr (HAS_B) pb[j] = mul4(*reinterpret_cast<const float4 *>(b + e), xv);
+            pa[j] = mul4(ld_stream(a + e), xv);  // A, B streamed once; x stays cached
+            if constexpr (HAS_B) pb[j] = mul4(ld_stream(b + e), xv);
         }
         const bool valid = cbase + lane < nchunks;
         // every lane writes slots of other lanes' chunks: transpose on all
