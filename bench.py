@@ -12,15 +12,20 @@ RCCL over xGMI, overlapped with the interior sweep.  Inputs are resident in
 HBM before the timed region; the timed region is exactly K steps bracketed by
 a barrier + device synchronize on both sides; the time is the max over ranks.
 
+A run of T steps is planned as T // 12 passes of the 12-step sweep plus one
+pass of the remainder (e.g. 20 = 12 + 8; config.plan).  Before the timed
+region every kernel of that plan launches once and untimed K-step passes run
+for at least --warmup-ms (GPU clock settling).
+
 The JSON line also carries:
-  roofline      -- the dominant sweep kernel (the K-step sweepk_kernel by
-                   default, K = 12 Jacobi steps per pass over HBM): algorithmic
+  roofline      -- the stencil kernel with the largest measured time in the
+                   timed region (HIP events around every launch, on the launch
+                   stream) and every kernel's share of the region: algorithmic
                    8 B/cell/step x cells x K per launch divided by its average
-                   duration (HIP events around every launch, on the launch
-                   stream, inside the timed region), vs the 8 TB/s HBM3E peak
-                   -- above 1 because of temporal blocking; `traffic` is the
-                   HBM bytes per launch from the rocprofv3 PMC passes committed
-                   under profiles/ and `hbm_frac` = traffic / launch time / peak
+                   duration, vs the 8 TB/s HBM3E peak -- above 1 because of
+                   temporal blocking; `traffic` is the HBM bytes per launch
+                   from the rocprofv3 PMC passes committed under profiles/ and
+                   `hbm_frac` = traffic / launch time / peak
   cpu_baseline  -- the oracle's C restatement of the reference stencil
                    (OpenMP) timed on this host on a bounded sample (rank 0,
                    N=1 only)
@@ -56,6 +61,18 @@ XGMI_LINK_GBS = 153.6          # MI355X Infinity Fabric: 7 links x 153.6 GB/s pe
 GESUMMV_N = 32768              # BASELINE config 5
 COLL_BYTES = (4 << 10, 1 << 20, 64 << 20, 256 << 20)   # BASELINE config 4 span
 AUX_BUDGET_S = 120.0           # watchdog on the auxiliary measurements
+WARMUP_MS = 50.0               # untimed warm-up floor (GPU clock settling)
+
+
+def kernel_label(kind: int, tag: int) -> str:
+    from smi_amd import profiling
+    if kind == profiling.SWEEPK:
+        return f"sweepk_kernel<{tag}> (smi_amd/csrc/stencilk.h, {tag} Jacobi steps per launch)"
+    if kind == profiling.SWEEP and tag == 2:
+        return "sweep2_kernel (smi_amd/csrc/stencil2.hip, two Jacobi steps per launch)"
+    if kind == profiling.SWEEP:
+        return "sweep_kernel (smi_amd/csrc/stencil.hip, one Jacobi step per launch)"
+    return "ring kernels (halo-facing band: ringk/ring2/edge)"
 
 
 def decomposition(n: int) -> tuple[int, int]:
@@ -297,6 +314,8 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=2400)
     ap.add_argument("--warmup", type=int, default=2400)
     ap.add_argument("--tile", type=int, default=TILE)
+    ap.add_argument("--warmup-ms", type=float, default=WARMUP_MS,
+                    help="untimed warm-up floor in ms of K-step passes after the --warmup steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aux", action="store_true",
                     help="skip the gesummv / reduce / bcast lines measured after the timed stencil region")
@@ -336,17 +355,26 @@ def main() -> None:
 
     fusion = stencil.get_fusion()
     K = fusion["steps_per_pass"]
+    plan = stencil.plan(X, Y, PX, PY, rank, args.steps)
+    warm_ms = 0.0
     with torch.cuda.stream(stream):
         if args.warmup:
             stencil.run(comm, tile, args.warmup, PX, PY, scratch)
-            # HIP loads a kernel's code object at its first launch: make sure
-            # every kernel of the timed run (K-step passes and the remainder's
-            # pair/single steps) has launched once outside the timed region
-            if K >= 4 and args.warmup < K <= args.steps:
-                stencil.run(comm, tile, K, PX, PY, scratch)
-            if args.steps % K:
-                stencil.run(comm, tile, args.steps % K, PX, PY, scratch)
+        # HIP loads a kernel's code object at its first launch: every kernel
+        # of the timed plan (the K-step passes and the remainder pass) runs
+        # once outside the timed region ...
+        for k, _ in plan["phases"]:
+            stencil.run(comm, tile, k, PX, PY, scratch)
         torch.cuda.synchronize()
+        # ... and the GPU clock needs tens of ms of load to settle (120 steps
+        # after 10 warm-up steps read ~11 % low, profiles/r01f/
+        # bench_warmup_sweep.log): untimed K-step passes until at least
+        # --warmup-ms of warm-up has run
+        t_w = time.perf_counter()
+        while (time.perf_counter() - t_w) * 1e3 < args.warmup_ms:
+            stencil.run(comm, tile, max(K, 1) * 4, PX, PY, scratch)
+            torch.cuda.synchronize()
+        warm_ms = (time.perf_counter() - t_w) * 1e3
         barrier()
         torch.cuda.synchronize()
         profiling.reset()
@@ -358,37 +386,44 @@ def main() -> None:
         t1 = time.perf_counter()
         profiling.enable(False)
     elapsed = t1 - t0
-    # the dominant kernel: the K-step sweep when the run has K-step passes
-    deep = K >= 4 and args.steps >= K and min(X, Y) >= 2 * K
-    spl = K if deep else (2 if K >= 2 and args.steps >= 2 else 1)  # steps per launch
-    sweep_ms, sweep_n = profiling.read(profiling.SWEEPK if deep else profiling.SWEEP)
-    edge_ms, edge_n = profiling.read(profiling.EDGE)
-    if world > 1:
-        t = torch.tensor([elapsed, sweep_ms], dtype=torch.float64)
+    # Every stencil kernel launched in the timed region, with its measured
+    # time (HIP events around each launch on its own stream); the roofline
+    # prices the one that took the most time.
+    kernels = []
+    for kern, tag in profiling.entries():
+        if kern not in (profiling.SWEEP, profiling.SWEEPK, profiling.EDGE):
+            continue
+        ms, n, units = profiling.read_tag(kern, tag)
+        kernels.append({"kernel": kernel_label(kern, tag), "kind": kern, "tag": tag, "launches": n,
+                        "total_ms": ms, "cell_steps": units})
+    if world > 1:  # the slowest rank's times, kernel by kernel (same plan on every rank)
+        t = torch.tensor([elapsed] + [k["total_ms"] for k in kernels], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, sweep_ms = float(t[0]), float(t[1])
-    sweep_avg_ms = sweep_ms / max(sweep_n, 1)
+        elapsed = float(t[0])
+        for i, k in enumerate(kernels):
+            k["total_ms"] = float(t[i + 1])
+    timed_ms = elapsed * 1e3
+    for k in kernels:
+        k["avg_ms"] = k["total_ms"] / max(k["launches"], 1)
+        k["share_of_timed_region"] = k["total_ms"] / timed_ms
+        k["algorithmic_GBs"] = (BYTES_PER_CELL * k["cell_steps"] / (k["total_ms"] * 1e-3) / 1e9
+                                if k["total_ms"] > 0 and k["cell_steps"] else None)
+    sweeps = [k for k in kernels if k["kind"] != profiling.EDGE]
+    dom = max(sweeps, key=lambda k: k["total_ms"]) if sweeps else None
 
     cells_per_gpu = X * Y
     total_cells = cells_per_gpu * world
     value = total_cells * args.steps / elapsed / 1e9
-    # Cells one launch of the dominant kernel computes: the whole tile, or in
-    # multi-rank runs the interior rectangle that stays clear of the ring the
-    # ring kernel computes (rank 0's tile).  Algorithmic bytes per launch =
-    # 8 B/cell/step x cells x steps per launch; with temporal blocking a launch
-    # carries K steps of algorithmic traffic while moving ~8 B/cell through
-    # HBM once (`traffic`, `hbm_achieved`).
-    ring = spl if spl >= 2 else 1
-    ipx, ipy = 0, 0
-    rows_c = X - ring * ((ipx > 0) + (ipx < PX - 1)) if world > 1 else X
-    cols_c = Y - ring * ((ipy > 0) + (ipy < PY - 1)) if world > 1 else Y
-    cells_launch = rows_c * cols_c
-    bytes_launch = BYTES_PER_CELL * cells_launch * spl
-    achieved = bytes_launch / (sweep_avg_ms * 1e-3) / 1e9 if sweep_n else 0.0
-    traffic = pmc_traffic(cells_per_gpu, spl) if world == 1 else None
-    kernel_name = {1: "sweep_kernel (smi_amd/csrc/stencil.hip)",
-                   2: "sweep2_kernel (smi_amd/csrc/stencil2.hip, two Jacobi steps per launch)"}.get(
-        spl, f"sweepk_kernel<{spl}> (smi_amd/csrc/stencilk.hip, {spl} Jacobi steps per launch)")
+    if dom:
+        spl = dom["tag"]  # steps per launch
+        cells_launch = int(round(dom["cell_steps"] / max(dom["launches"], 1) / spl))
+        bytes_launch = BYTES_PER_CELL * cells_launch * spl
+        sweep_avg_ms = dom["avg_ms"]
+        achieved = bytes_launch / (sweep_avg_ms * 1e-3) / 1e9
+        kernel_name = dom["kernel"]
+    else:
+        spl, cells_launch, bytes_launch, sweep_avg_ms, achieved, kernel_name = 0, 0, 0, 0.0, 0.0, None
+    traffic = pmc_traffic(cells_per_gpu, spl) if world == 1 and dom else None
     out = {
         "metric": "Jacobi stencil GCell/s (8192^2 fp32 per GPU)",
         "value": round(value, 2),
@@ -410,8 +445,11 @@ def main() -> None:
             "grid": [PX * X, PY * Y],
             "tile": [X, Y],
             "decomposition": [PX, PY],
+            "plan": [{"steps_per_pass": k, "passes": n} for k, n in plan["phases"]],
             "tuning": stencil.get_tuning(),
             "fusion": fusion,
+            "warmup_ms_floor": args.warmup_ms,
+            "warmup_ms_run": round(warm_ms, 1),
         },
         "roofline": {
             "bound": "hbm",
@@ -422,24 +460,29 @@ def main() -> None:
             "traffic": traffic,
             "kernel": kernel_name,
             "kernel_avg_ms": round(sweep_avg_ms, 5),
-            "launches": sweep_n,
+            "launches": dom["launches"] if dom else 0,
             "steps_per_launch": spl,
             "cells_per_launch": cells_launch,
             "bytes_per_launch": int(bytes_launch),
-            "note": "achieved = algorithmic 8 B/cell/step x steps per launch / avg launch time (HIP events); "
-                    "frac > 1 is temporal blocking: K steps per pass over HBM. traffic = measured HBM bytes "
-                    "per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE); hbm_frac = traffic / avg launch time "
-                    "/ peak is the memory system's utilisation",
+            "share_of_timed_region": round(dom["share_of_timed_region"], 4) if dom else None,
+            "kernels": [{"kernel": k["kernel"], "launches": k["launches"], "total_ms": round(k["total_ms"], 5),
+                         "avg_ms": round(k["avg_ms"], 5), "share_of_timed_region": round(k["share_of_timed_region"], 4),
+                         "algorithmic_GBs": round(k["algorithmic_GBs"], 1) if k["algorithmic_GBs"] else None}
+                        for k in kernels],
+            "note": "kernel = the stencil kernel with the largest measured time in the timed region (HIP events "
+                    "around every launch, on its stream); achieved = algorithmic 8 B/cell/step x steps per launch "
+                    "/ its avg launch time; frac > 1 is temporal blocking: K steps per pass over HBM. traffic = "
+                    "measured HBM bytes per launch of that kernel (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                    "profiles/pmc_stencil_sweep.json); hbm_frac = traffic / avg launch time / peak is the memory "
+                    "system's utilisation",
         },
     }
-    if traffic and sweep_n:
+    if traffic and sweep_avg_ms:
         hbm = traffic / (sweep_avg_ms * 1e-3) / 1e9
         out["roofline"]["hbm_achieved"] = round(hbm, 1)
         out["roofline"]["hbm_frac"] = round(hbm / HBM_PEAK_GBS, 4)
-    if edge_n:
-        out["roofline"]["edge_kernel_avg_ms"] = round(edge_ms / edge_n, 5)
     if world > 1:
-        out["halo"] = halo_report(PX, PY, X, Y, spl if deep else 1, elapsed / args.steps * 1e3)
+        out["halo"] = halo_report(PX, PY, X, Y, max(spl, 1), elapsed / args.steps * 1e3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
 

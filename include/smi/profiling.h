@@ -30,6 +30,13 @@ int smi_prof_reset(void);
 /* Synchronises the recorded events; *total_ms = summed kernel time,
  * *launches = number of timed launches of `kernel`. */
 int smi_prof_read(int kernel, double *total_ms, long *launches);
+/* The same for launches recorded with `tag` (-1: any tag; the K-step sweep
+ * tags each launch with its K); *units (nullable) = their summed
+ * algorithmic work: cell-steps for the stencil kernels. */
+int smi_prof_read_tag(int kernel, int tag, double *total_ms, long *launches, double *units);
+/* Distinct (kernel, tag) pairs recorded since the last reset, in first-seen
+ * order: up to max_entries written, *n_entries = how many exist. */
+int smi_prof_list(int *kernels, int *tags, int max_entries, int *n_entries);
 
 #ifdef __cplusplus
 }

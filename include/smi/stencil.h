@@ -67,20 +67,38 @@ int smi_stencil_set_tuning(int rows_per_wave, int rows_in_flight,
 int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
                            int *nontemporal_stores, int *overlap);
 
-/* Temporal blocking: steps_per_pass = K in {2, 4, 8, 12} fuses K Jacobi
- * steps into one pass over HBM (same per-cell arithmetic, bit-identical
- * result).  Multi-rank runs then exchange depth-K halos -- K rows/columns per
- * side neighbour and a K x K corner block per diagonal neighbour -- once per
- * K steps; a ring kernel computes the K-wide halo-facing band while the
- * interior sweep runs.  Default K = 12.  The bulk of a run uses K-step
- * passes, the remainder (timesteps % K) pairs and then single steps; tiles
- * smaller than 2K x 2K in a multi-rank run skip the K-step passes, tiles
- * smaller than 4 x 8 run single steps only.
- * rows_per_wave: rows per wave of the active fused kernel (K >= 4: -1 =
+/* Temporal blocking: steps_per_pass = K in 1..12 fuses up to K Jacobi steps
+ * into one pass over HBM (same per-cell arithmetic, bit-identical result).
+ * Multi-rank runs then exchange depth-K halos -- K rows/columns per side
+ * neighbour and a K x K corner block per diagonal neighbour -- once per K
+ * steps; a ring kernel computes the K-wide halo-facing band while the
+ * interior sweep runs.  Default K = 12.  A run is planned as K-step passes,
+ * then ONE pass of the remainder r = timesteps % K when r >= 3, else a pair
+ * and/or a single step (smi_stencil_plan).  In a multi-rank run K is
+ * clipped to half the smaller tile side; tiles smaller than 4 x 8 run single
+ * steps only.
+ * rows_per_wave: rows per wave of the active fused kernel (K >= 3: -1 =
  * automatic, one round of resident waves); rows_in_flight (1, 2, 4 or 8)
- * tunes the two-step kernel and is ignored for K >= 4.  Pass 0 to keep. */
+ * tunes the two-step kernel and is ignored for K >= 3.  Pass 0 to keep. */
 int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_flight);
 int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in_flight);
+
+/* One phase of a planned run: `passes` launches of `steps_per_pass` steps. */
+typedef struct {
+    int steps_per_pass;
+    int passes;
+} SMI_StencilPhase;
+
+/* The schedule smi_stencil_run follows on `rank` of a px x py decomposition
+ * of x_local x y_local tiles under the current fusion setting, computed on
+ * the host (no device needed): the phases in order (4 always suffice), the
+ * neighbour ranks top, bottom, left, right, top-left, top-right,
+ * bottom-left, bottom-right (-1 on the global edge; nullable; the rank map
+ * of stencil_smi.cpp:133-134) and the index of the buffer that will hold
+ * the result (nullable). */
+int smi_stencil_plan(int x_local, int y_local, int px, int py, int rank, int timesteps,
+                     SMI_StencilPhase *phases, int max_phases, int *nphases, int neighbours[8],
+                     int *result_index);
 
 #ifdef __cplusplus
 }

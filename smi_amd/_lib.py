@@ -78,6 +78,10 @@ SIGNATURES = {
     "smi_prof_enable": (I, [I]),
     "smi_prof_reset": (I, []),
     "smi_prof_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),
+    "smi_prof_read_tag": (I, [I, I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long),
+                              ctypes.POINTER(ctypes.c_double)]),
+    "smi_prof_list": (I, [ctypes.POINTER(I), ctypes.POINTER(I), I, ctypes.POINTER(I)]),
+    "smi_stencil_plan": (I, [I, I, I, I, I, I, P, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)]),
 }
 
 

@@ -28,10 +28,28 @@ CXXFLAGS = [
     f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
     f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
 ]
-# Per-file extras.  stencilk.hip spells out which adds are packed
+# Per-file extras (by file-name prefix).  The K-step sweep (stencilk.h,
+# instantiated in stencilk_k<K>.hip) spells out which adds are packed
 # (v_pk_add_f32 on aligned pairs); the SLP vectorizer would pack the
 # shuffled (S+W)/(+E) adds too and pay a register move for each pair.
-FILE_FLAGS = {"stencilk.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"stencilk_k": ["-fno-slp-vectorize"]}
+# Build variants: the product library, a bounds-checked diagnostic build, the
+# loopback rehearsal build (tools/rehearsal.py) and timing experiments
+# (tools/sweep_experiment.py), each in its own directory.
+VARIANT_FLAGS = {
+    "": [],
+    "debug": ["-DSMI_BOUNDS_CHECK"],
+    "rehearsal": ["-DSMI_LOOPBACK_REHEARSAL"],
+    "exp_g1": ["-DSMI_SWEEPK_GROUPS=1"],
+    "exp_g3": ["-DSMI_SWEEPK_GROUPS=3"],
+    "exp_nt": ["-DSMI_SWEEPK_LOAD_AUX=2"],
+    "exp_onedir": ["-DSMI_EXP_ONE_DIRECTION"],
+}
+
+
+def file_flags(src: str) -> list[str]:
+    name = os.path.basename(src)
+    return [f for prefix, fl in FILE_FLAGS.items() if name.startswith(prefix) for f in fl]
 LDFLAGS = ["-shared", f"-L{ROCM}/lib", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"]
 
 
@@ -40,12 +58,12 @@ def sources() -> list[str]:
 
 
 def lib_path(variant: str = "") -> str:
-    """release: _build/libsmi_amd.so; "debug": bounds-checked diagnostic build."""
-    if variant == "debug":
-        return os.path.join(OUT_DIR, "debug", "libsmi_amd_debug.so")
-    if variant == "rehearsal":
-        return os.path.join(OUT_DIR, "rehearsal", "libsmi_amd_rehearsal.so")
-    return LIB
+    """release: _build/libsmi_amd.so; otherwise _build/<variant>/libsmi_amd_<variant>.so."""
+    if not variant:
+        return LIB
+    if variant not in VARIANT_FLAGS:
+        raise ValueError(f"unknown build variant {variant!r}")
+    return os.path.join(OUT_DIR, variant, f"libsmi_amd_{variant}.so")
 
 
 def _stale(variant: str = "") -> bool:
@@ -64,14 +82,13 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
         return lib
     out_dir = os.path.dirname(lib)
     os.makedirs(out_dir, exist_ok=True)
-    flags = CXXFLAGS + {"debug": ["-DSMI_BOUNDS_CHECK"],
-                        "rehearsal": ["-DSMI_LOOPBACK_REHEARSAL"]}.get(variant, [])
+    flags = CXXFLAGS + VARIANT_FLAGS[variant]
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     objs = []
     procs = []
     for src in sources():
         obj = os.path.join(out_dir, os.path.basename(src) + ".o")
-        cmd = [hipcc, *flags, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
+        cmd = [hipcc, *flags, *file_flags(src), "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
@@ -93,5 +110,5 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True,
-                variant="debug" if "--debug" in sys.argv else ("rehearsal" if "--rehearsal" in sys.argv else "")))
+    v = next((a[2:] for a in sys.argv[1:] if a.startswith("--") and a[2:] in VARIANT_FLAGS), "")
+    print(build(force="--force" in sys.argv, verbose=True, variant=v))

@@ -85,6 +85,8 @@ static int finish_init(std::unique_ptr<Comm> c, SMI_Comm *out) {
 // ------------------------------------------------------------ profiling --
 struct ProfRec {
     int kernel;
+    int tag;
+    double units;
     hipEvent_t a, b;
 };
 static std::mutex g_prof_mu;
@@ -107,10 +109,12 @@ static int prof_get_event(hipEvent_t *e) {
     return SMI_SUCCESS;
 }
 
-int prof_begin(int kernel, hipStream_t stream, int *token) {
+int prof_begin(int kernel, hipStream_t stream, int *token, int tag, double units) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     ProfRec r;
     r.kernel = kernel;
+    r.tag = tag;
+    r.units = units;
     SMI_TRY(prof_get_event(&r.a));
     SMI_TRY(prof_get_event(&r.b));
     SMI_HIP_CHECK(hipEventRecord(r.a, stream));
@@ -233,20 +237,44 @@ int smi_prof_reset(void) {
 }
 
 int smi_prof_read(int kernel, double *total_ms, long *launches) {
+    return smi_prof_read_tag(kernel, -1, total_ms, launches, nullptr);
+}
+
+int smi_prof_read_tag(int kernel, int tag, double *total_ms, long *launches, double *units) {
     SMI_ARG_CHECK(total_ms && launches, "NULL output");
     std::lock_guard<std::mutex> lk(g_prof_mu);
-    double sum = 0.0;
+    double sum = 0.0, u = 0.0;
     long n = 0;
     for (auto &r : g_prof_recs) {
-        if (r.kernel != kernel) continue;
+        if (r.kernel != kernel || (tag >= 0 && r.tag != tag)) continue;
         SMI_HIP_CHECK(hipEventSynchronize(r.b));
         float ms = 0.f;
         SMI_HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
         sum += ms;
+        u += r.units;
         ++n;
     }
     *total_ms = sum;
     *launches = n;
+    if (units) *units = u;
+    return SMI_SUCCESS;
+}
+
+int smi_prof_list(int *kernels, int *tags, int max_entries, int *n_entries) {
+    SMI_ARG_CHECK(n_entries && (max_entries == 0 || (kernels && tags)), "NULL output");
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    int n = 0;
+    for (auto &r : g_prof_recs) {
+        bool seen = false;
+        for (int i = 0; i < n && i < max_entries; ++i) seen |= kernels[i] == r.kernel && tags[i] == r.tag;
+        if (seen) continue;
+        if (n < max_entries) {
+            kernels[n] = r.kernel;
+            tags[n] = r.tag;
+        }
+        ++n;
+    }
+    *n_entries = n;
     return SMI_SUCCESS;
 }
 

@@ -222,7 +222,7 @@ int launch_sweep(const SweepArgs &a, hipStream_t s) {
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
     int tok = -1;
-    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEP, s, &tok));
+    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEP, s, &tok, 1, (double)a.rows * a.cols));
     switch (g_tune.u) {
     case 1: launch_sweep_u<1>(a, nstrips, nrb, ht, blocks, g_tune.nt, s); break;
     case 2: launch_sweep_u<2>(a, nstrips, nrb, ht, blocks, g_tune.nt, s); break;

@@ -315,7 +315,7 @@ int launch_sweep2(const Sweep2Args &a, hipStream_t s) {
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
     int tok = -1;
-    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEP, s, &tok));
+    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEP, s, &tok, 2, 2.0 * (hi - lo) * a.cols));
     switch (g_tune.u2) {
     case 1: launch_sweep2_u<1>(a, nstrips, nrb, ht, blocks, lo, hi, g_tune.nt, s); break;
     case 2: launch_sweep2_u<2>(a, nstrips, nrb, ht, blocks, lo, hi, g_tune.nt, s); break;

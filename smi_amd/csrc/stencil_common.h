@@ -65,7 +65,7 @@ struct Tuning {
     int u = 16;         // rows in flight per batch
     int nt = 1;         // non-temporal stores
     int overlap = 1;    // overlap halo exchange with the interior sweep
-    int fuse = 12;      // Jacobi steps per pass over HBM (1, 2, 4, 8 or 12)
+    int fuse = 12;      // Jacobi steps per pass over HBM (1..12; the remainder runs as one shallower pass)
     int ht2 = 8;        // rows per wave (two-step sweep)
     int u2 = 8;         // rows in flight per batch (two-step sweep)
     int htk = 0;        // rows per wave (K-step sweep, K >= 4); 0 = one round of resident waves
@@ -76,7 +76,7 @@ struct Tuning {
     // where workgroups retire, so the RCCL kernel of the exchange is never
     // left without a slot until the interior ends.
     int rounds_multi = 2;
-    int uk = 3;         // rows per load batch (K-step sweep: fixed at 3, the slot ring period)
+    int uk = 6;         // rows loaded ahead (K-step sweep: fixed at build time, SMI_SWEEPK_D)
 };
 extern Tuning g_tune;
 
@@ -108,7 +108,7 @@ int launch_sweep2(const Sweep2Args &a, hipStream_t s);
 int launch_ring2(const Sweep2Args &a, const Halo2 &h, hipStream_t s);
 int launch_pack2(const float *in, int rows, int cols, const Halo2 &h, hipStream_t s);
 
-// K steps per pass (stencilk.hip, K = 4 or 8): output rectangle
+// K steps per pass (stencilk.hip, 3 <= K <= 12): output rectangle
 // [row_lo,row_hi) x [col_lo,col_hi) of the tile, computed from input cells
 // within K of it (all inside the tile); g* = 1 where the side is a global
 // edge of the grid (its outermost row/column is copied every step).
@@ -119,7 +119,20 @@ struct SweepKArgs {
     int row_lo, row_hi, col_lo, col_hi;
     int gT, gB, gL, gR;
 };
+constexpr int SWEEPK_MIN = 3, SWEEPK_MAX = 12;
+// How a K-step row block [o0, o1) meets the global edge rows: 0 its cone
+// never reaches one (fast kernel), 1 holds row 0 only, 2 holds row X-1 only,
+// 3 otherwise; anything but 0 takes the FULL kernel (stencilk.h).  The cone
+// spans rows [o0 - K, o1 + K); the margins are generous.
+__host__ __device__ inline int sweepk_row_class(const SweepKArgs &a, int K, int o0, int o1) {
+    const bool touchT = a.gT && o0 - 2 * K <= 0;
+    const bool touchB = a.gB && o1 + K + 6 >= a.rows;
+    if (touchT && !touchB && o0 == 0) return 1;
+    if (touchB && !touchT && o1 == a.rows) return 2;
+    return (touchT || touchB) ? 3 : 0;
+}
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s);
+int sweepk_window_cols(int K);  // output columns per 256-column window
 
 // Depth-K halos (stencil_ringk.hip).  Receive side: top = rows -K..-1 and
 // bot = rows X..X+K-1 (K x Y, row-major), left = cols -K..-1 and right =
@@ -134,14 +147,18 @@ struct HaloK {
     float *send_left, *send_right;
     float *send_corner[4];
 };
+constexpr int RING_KMAX = 12;
 constexpr int RB_H = 64;  // ring block rows (left/right bands)
 constexpr int RB_W = 64;  // ring block columns (top/bottom bands)
 struct RingKArgs {
     const float *in;
     float *out;
     int rows, cols, k;
+    int bandw;         // left/right band width: K rounded up to float4 columns (set by launch_ringk)
     int has[4];        // neighbour on side top, bottom, left, right
     int has_diag[4];   // neighbour tl, tr, bl, br
+    int band[4];       // compute the band of side k (halo side, or a global edge column)
+    int pack;          // write the next exchange's sends (multi-rank)
     HaloK h;
     // filled by launch_ringk: band rectangles and block prefix
     int r0[4], r1[4], c0[4], c1[4];

@@ -1,4 +1,5 @@
-// stencil_ringk.hip -- the halo-facing ring of a K-step pass (K = 4, 8, 12).
+// stencil_ringk.hip -- the halo-facing ring of a K-step pass (3 <= K <= 12),
+// and the global edge-column bands of any K-step pass.
 //
 // In a multi-rank run with K Jacobi steps per pass, every tile cell within K
 // of a side that has a neighbour depends on that neighbour's cells (up to K
@@ -40,19 +41,21 @@ __device__ __forceinline__ float ext_at(const RingKArgs &a, int p, int q) {
 }
 
 // Output blocks: top/bottom bands in K x RB_W blocks, left/right bands in
-// RB_H x K blocks (block b -> band via the prefix table in RingKArgs).
-template <int K>
+// RB_H x K blocks (block b -> band via the prefix table in RingKArgs).  K is
+// a runtime value (the depth of the current phase); LDS is sized for
+// RING_KMAX.
 __global__ __launch_bounds__(256) void ringk_kernel(RingKArgs a) {
     // horizontal blocks: 3K x (RB_W + 2K); vertical blocks: (RB_H + 2K) x 3K
-    constexpr int LDS_N = 3 * K * ((RB_W > RB_H ? RB_W : RB_H) + 2 * K);
+    constexpr int LDS_N = 3 * RING_KMAX * ((RB_W > RB_H ? RB_W : RB_H) + 2 * RING_KMAX);
     __shared__ float lds[2][LDS_N];
+    const int K = a.k;
     const int b = blockIdx.x;
     int band = 0;
     while (band < 3 && b >= a.first_block[band + 1]) ++band;
     const int lb = b - a.first_block[band];
     const int r0 = a.r0[band], r1 = a.r1[band], c0 = a.c0[band], c1 = a.c1[band];
     const bool horiz = band < 2;  // top/bottom band: K rows x wide
-    const int bh = horiz ? K : RB_H, bw = horiz ? RB_W : K;
+    const int bh = horiz ? K : RB_H, bw = horiz ? RB_W : a.bandw;
     const int nbc = (c1 - c0 + bw - 1) / bw;
     const int oR0 = r0 + (lb / nbc) * bh, oC0 = c0 + (lb % nbc) * bw;
     const int oR1 = min(oR0 + bh, r1), oC1 = min(oC0 + bw, c1);
@@ -87,6 +90,7 @@ __global__ __launch_bounds__(256) void ringk_kernel(RingKArgs a) {
         const int p = oR0 + y, q = oC0 + x;
         const float v = res[(y + K) * W + (x + K)];
         a.out[(size_t)p * Y + q] = v;
+        if (!a.pack) continue;
         if (q < K) a.h.send_left[(size_t)p * K + q] = v;
         if (q >= Y - K) a.h.send_right[(size_t)p * K + (q - (Y - K))] = v;
         if (p < K || p >= X - K) {
@@ -119,13 +123,19 @@ __global__ __launch_bounds__(256) void packk_kernel(const float *in, int X, int 
 
 int launch_ringk(RingKArgs a, hipStream_t s) {
     const int X = a.rows, Y = a.cols, K = a.k;
-    SMI_ARG_CHECK(K == 4 || K == 8 || K == 12, "ring: K must be 4, 8 or 12");
-    SMI_ARG_CHECK(X >= 2 * K && Y >= 2 * K, "ring: tile smaller than 2K");
+    // left/right bands are K rounded up to whole float4 columns wide, so the
+    // interior sweep's column range stays 16-byte aligned
+    const int W = 4 * ((K + 3) / 4);
+    a.bandw = W;
+    SMI_ARG_CHECK(K >= 1 && K <= RING_KMAX, "ring: K must be 1..12");
+    SMI_ARG_CHECK(X >= 2 * K && Y >= 2 * W, "ring: tile smaller than 2K x 2W");
     // bands: top rows [0,K), bottom rows [X-K,X) (full width); left/right
-    // columns over the rows the top/bottom bands leave
-    const int rlo = a.has[0] ? K : 0, rhi = a.has[1] ? X - K : X;
+    // columns [0,W) / [Y-W,Y) over the rows the top/bottom bands leave.
+    // band[k]: side k facing a halo, or a global edge column the interior
+    // sweep leaves to this kernel (its copy rule, stencil_smi.cl:143-151)
+    const int rlo = a.band[0] ? K : 0, rhi = a.band[1] ? X - K : X;
     const int band_r0[4] = {0, X - K, rlo, rlo}, band_r1[4] = {K, X, rhi, rhi};
-    const int band_c0[4] = {0, 0, 0, Y - K}, band_c1[4] = {Y, Y, K, Y};
+    const int band_c0[4] = {0, 0, 0, Y - W}, band_c1[4] = {Y, Y, W, Y};
     int nb = 0;
     for (int k = 0; k < 4; ++k) {
         a.r0[k] = band_r0[k];
@@ -133,20 +143,16 @@ int launch_ringk(RingKArgs a, hipStream_t s) {
         a.c0[k] = band_c0[k];
         a.c1[k] = band_c1[k];
         a.first_block[k] = nb;
-        if (!a.has[k] || a.r1[k] <= a.r0[k]) continue;
+        if (!a.band[k] || a.r1[k] <= a.r0[k]) continue;
         const bool horiz = k < 2;
-        const int bh = horiz ? K : RB_H, bw = horiz ? RB_W : K;
+        const int bh = horiz ? K : RB_H, bw = horiz ? RB_W : W;
         nb += ((a.r1[k] - a.r0[k] + bh - 1) / bh) * ((a.c1[k] - a.c0[k] + bw - 1) / bw);
     }
     a.first_block[4] = nb;
     if (nb == 0) return SMI_SUCCESS;
     int tok = -1;
     if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_EDGE, s, &tok));
-    switch (K) {
-    case 4: hipLaunchKernelGGL(ringk_kernel<4>, dim3(nb), dim3(256), 0, s, a); break;
-    case 8: hipLaunchKernelGGL(ringk_kernel<8>, dim3(nb), dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(ringk_kernel<12>, dim3(nb), dim3(256), 0, s, a); break;
-    }
+    hipLaunchKernelGGL(ringk_kernel, dim3(nb), dim3(256), 0, s, a);
     SMI_HIP_CHECK(hipGetLastError());
     if (tok >= 0) SMI_TRY(prof_end(tok, s));
     return SMI_SUCCESS;

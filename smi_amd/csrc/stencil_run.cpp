@@ -168,6 +168,68 @@ static int ensure_halo(Comm *c, size_t elems) {
     return SMI_SUCCESS;
 }
 
+static Neighbours neighbours_of(int rank, int px, int py) {
+    // rank -> (i_px, i_py), examples/host/stencil_smi.cpp:133-134
+    const int ipx = rank / py, ipy = rank % py;
+    Neighbours nb;
+    if (ipx > 0) nb.top = (ipx - 1) * py + ipy;
+    if (ipx < px - 1) nb.bottom = (ipx + 1) * py + ipy;
+    if (ipy > 0) nb.left = ipx * py + ipy - 1;
+    if (ipy < py - 1) nb.right = ipx * py + ipy + 1;
+    if (nb.top >= 0 && nb.left >= 0) nb.tl = (ipx - 1) * py + ipy - 1;
+    if (nb.top >= 0 && nb.right >= 0) nb.tr = (ipx - 1) * py + ipy + 1;
+    if (nb.bottom >= 0 && nb.left >= 0) nb.bl = (ipx + 1) * py + ipy - 1;
+    if (nb.bottom >= 0 && nb.right >= 0) nb.br = (ipx + 1) * py + ipy + 1;
+    return nb;
+}
+
+// The phases of a run: K-step passes of the configured K (clipped to what the
+// tile holds: a multi-rank tile needs 2K x 2K), then ONE pass of the
+// remainder when it is 3 or more steps, else a pair and/or a single step.
+// Every phase starts from halos of the current state, so the split changes
+// scheduling only, never a bit of the result.
+struct Plan {
+    int nph = 0;
+    int k[4] = {0, 0, 0, 0};  // steps per pass
+    int n[4] = {0, 0, 0, 0};  // passes
+    int passes() const { return n[0] + n[1] + n[2] + n[3]; }
+};
+
+static Plan make_plan(int rows, int cols, int timesteps, bool multi) {
+    Plan p;
+    auto add = [&](int k, int n) {
+        if (n > 0) {
+            p.k[p.nph] = k;
+            p.n[p.nph] = n;
+            ++p.nph;
+        }
+    };
+    const int fuse = g_tune.fuse;
+    int K = fuse >= SWEEPK_MIN ? fuse : 0;
+    if (K && multi) {
+        // a multi-rank tile holds the K-row bands and the float4-aligned
+        // K-column bands (4 * ceil(K / 4) wide) of both sides
+        K = std::min(K, rows / 2);
+        while (K > 0 && 8 * ((K + 3) / 4) > cols) --K;
+    }
+    if (cols < 8 || K < SWEEPK_MIN) K = 0;
+    int rest = timesteps;
+    if (K) {
+        add(K, rest / K);
+        rest %= K;
+        if (rest >= SWEEPK_MIN) {
+            add(rest, 1);
+            rest = 0;
+        }
+    }
+    if (fuse >= 2 && rows >= 4 && cols >= 8) {
+        add(2, rest / 2);
+        rest %= 2;
+    }
+    add(1, rest);
+    return p;
+}
+
 }  // namespace smi
 
 using namespace smi;
@@ -176,13 +238,11 @@ extern "C" {
 
 int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_flight) {
     if (steps_per_pass > 0) {
-        SMI_ARG_CHECK(steps_per_pass == 1 || steps_per_pass == 2 || steps_per_pass == 4 || steps_per_pass == 8 ||
-                          steps_per_pass == 12,
-                      "steps_per_pass must be 1, 2, 4, 8 or 12");
+        SMI_ARG_CHECK(steps_per_pass <= SWEEPK_MAX, "steps_per_pass must be 1..12");
         g_tune.fuse = steps_per_pass;
     }
     // rows_per_wave / rows_in_flight tune the kernel of the current setting
-    const bool deep = g_tune.fuse >= 4;
+    const bool deep = g_tune.fuse >= SWEEPK_MIN;
     if (rows_per_wave > 0) (deep ? g_tune.htk : g_tune.ht2) = rows_per_wave;
     if (rows_per_wave < 0 && deep) g_tune.htk = 0;  // automatic: one round of resident waves
     if (rows_in_flight > 0 && !deep) {
@@ -190,16 +250,39 @@ int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_fl
                       "rows_in_flight must be 1, 2, 4 or 8");
         g_tune.u2 = rows_in_flight;
     }
-    // the K-step sweep loads in batches of 3 rows (its slot-ring period);
+    // the K-step sweep's pipeline depth is fixed at build time;
     // rows_in_flight is accepted and ignored there
     return SMI_SUCCESS;
 }
 
 int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in_flight) {
-    const bool deep = g_tune.fuse >= 4;
+    const bool deep = g_tune.fuse >= SWEEPK_MIN;
     if (steps_per_pass) *steps_per_pass = g_tune.fuse;
     if (rows_per_wave) *rows_per_wave = deep ? g_tune.htk : g_tune.ht2;
     if (rows_in_flight) *rows_in_flight = deep ? g_tune.uk : g_tune.u2;
+    return SMI_SUCCESS;
+}
+
+int smi_stencil_plan(int x_local, int y_local, int px, int py, int rank, int timesteps, SMI_StencilPhase *phases,
+                     int max_phases, int *nphases, int *neighbours, int *result_index) {
+    SMI_ARG_CHECK(x_local >= 1 && y_local >= 4 && y_local % 4 == 0, "tile must be >= 1 x 4, y_local % 4 == 0");
+    SMI_ARG_CHECK(px >= 1 && py >= 1 && rank >= 0 && rank < px * py, "rank outside the px x py grid");
+    SMI_ARG_CHECK(timesteps >= 0, "timesteps < 0");
+    SMI_ARG_CHECK(nphases && (phases || max_phases == 0), "NULL output");
+    const Neighbours nb = neighbours_of(rank, px, py);
+    const bool multi = nb.top >= 0 || nb.bottom >= 0 || nb.left >= 0 || nb.right >= 0;
+    const Plan p = make_plan(x_local, y_local, timesteps, multi);
+    SMI_ARG_CHECK(max_phases >= p.nph, "max_phases too small (4 always suffice)");
+    for (int i = 0; i < p.nph; ++i) {
+        phases[i].steps_per_pass = p.k[i];
+        phases[i].passes = p.n[i];
+    }
+    *nphases = p.nph;
+    if (neighbours) {
+        const int v[8] = {nb.top, nb.bottom, nb.left, nb.right, nb.tl, nb.tr, nb.bl, nb.br};
+        for (int i = 0; i < 8; ++i) neighbours[i] = v[i];
+    }
+    if (result_index) *result_index = p.passes() & 1;
     return SMI_SUCCESS;
 }
 
@@ -217,17 +300,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     hipStream_t s = (hipStream_t)stream_;
     hipStream_t cs = c->comm_stream;
     const int rows = x_local, cols = y_local;
-    // rank -> (i_px, i_py), examples/host/stencil_smi.cpp:133-134
-    const int ipx = c->rank / py, ipy = c->rank % py;
-    Neighbours nb;
-    if (ipx > 0) nb.top = (ipx - 1) * py + ipy;
-    if (ipx < px - 1) nb.bottom = (ipx + 1) * py + ipy;
-    if (ipy > 0) nb.left = ipx * py + ipy - 1;
-    if (ipy < py - 1) nb.right = ipx * py + ipy + 1;
-    if (nb.top >= 0 && nb.left >= 0) nb.tl = (ipx - 1) * py + ipy - 1;
-    if (nb.top >= 0 && nb.right >= 0) nb.tr = (ipx - 1) * py + ipy + 1;
-    if (nb.bottom >= 0 && nb.left >= 0) nb.bl = (ipx + 1) * py + ipy - 1;
-    if (nb.bottom >= 0 && nb.right >= 0) nb.br = (ipx + 1) * py + ipy + 1;
+    Neighbours nb = neighbours_of(c->rank, px, py);
 #ifdef SMI_LOOPBACK_REHEARSAL
     // Timing-rehearsal build only (never the product library; built by
     // `smi_amd/build.py --rehearsal`, driven by tools/rehearsal.py): with
@@ -244,18 +317,11 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     for (int k = 0; k < 4; ++k)
         if (side_nb[k] >= 0) side_mask |= 1 << k;
 
-    // K steps per pass for the bulk (tiles of at least 2K x 2K when
-    // multi-rank), then pairs of steps, then single steps
-    int K = g_tune.fuse >= 4 ? g_tune.fuse : 0;
-    if (K && side_mask && (rows < 2 * K || cols < 2 * K)) K = 0;
-    if (K && cols < 8) K = 0;
-    const int kpasses = K ? timesteps / K : 0;
-    const int rest = timesteps - K * kpasses;
-    const bool fused = g_tune.fuse >= 2 && rows >= 4 && cols >= 8;
-    const int pairs = fused ? rest / 2 : 0;
-    const int singles = rest - 2 * pairs;
-    *result_index = (kpasses + pairs + singles) & 1;
+    const Plan plan = make_plan(rows, cols, timesteps, side_mask != 0);
+    *result_index = plan.passes() & 1;
     if (timesteps == 0) return SMI_SUCCESS;
+    int kmax = 0;  // deepest K-step phase (sizes the depth-K staging)
+    for (int i = 0; i < plan.nph; ++i) kmax = std::max(kmax, plan.k[i] >= SWEEPK_MIN ? plan.k[i] : 0);
 
     // single-step arguments (modes / halo views set below)
     SweepArgs a{};
@@ -266,47 +332,103 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     a2.rows = rows;
     a2.cols = cols;
     for (int k = 0; k < 4; ++k) a2.skip[k] = side_nb[k] >= 0;
-    // K-step interior: stays K cells clear of every halo-facing side
-    SweepKArgs ak{};
-    ak.rows = rows;
-    ak.cols = cols;
-    ak.row_lo = nb.top >= 0 ? K : 0;
-    ak.row_hi = nb.bottom >= 0 ? rows - K : rows;
-    ak.col_lo = nb.left >= 0 ? K : 0;
-    ak.col_hi = nb.right >= 0 ? cols - K : cols;
-    ak.gT = nb.top < 0;
-    ak.gB = nb.bottom < 0;
-    ak.gL = nb.left < 0;
-    ak.gR = nb.right < 0;
+    // K-step passes: the interior sweep stays K rows / 4*ceil(K/4) columns
+    // clear of every halo-facing side AND of the global edges (whose copy
+    // rule stencil_smi.cl:143-151 would cost the fast sweep a wave per SIMD,
+    // stencilk.h); the ring kernel computes those bands beside it.  Tiles too
+    // small for the bands run their global-edge sides through the sweep's
+    // FULL kernel.
+    auto kc_of = [](int K) { return 4 * ((K + 3) / 4); };
+    auto bands_ok = [&](int K) { return rows >= 4 * K && cols >= 4 * kc_of(K); };
+    auto interior_args = [&](int K) {
+        SweepKArgs ak{};
+        ak.rows = rows;
+        ak.cols = cols;
+        const bool bands = bands_ok(K);
+        const int kc = kc_of(K);
+        ak.row_lo = (nb.top >= 0 || bands) ? K : 0;
+        ak.row_hi = (nb.bottom >= 0 || bands) ? rows - K : rows;
+        ak.col_lo = (nb.left >= 0 || bands) ? kc : 0;
+        ak.col_hi = (nb.right >= 0 || bands) ? cols - kc : cols;
+        // a global edge inside the interior's cone only without bands
+        ak.gT = nb.top < 0 && !bands;
+        ak.gB = nb.bottom < 0 && !bands;
+        ak.gL = nb.left < 0 && !bands;
+        ak.gR = nb.right < 0 && !bands;
+        return ak;
+    };
+    const int diag_nb[4] = {nb.tl, nb.tr, nb.bl, nb.br};
+    auto ring_args = [&](int K) {
+        RingKArgs rk{};
+        rk.rows = rows;
+        rk.cols = cols;
+        rk.k = K;
+        for (int k = 0; k < 4; ++k) rk.has[k] = side_nb[k] >= 0;
+        for (int k = 0; k < 4; ++k) rk.has_diag[k] = diag_nb[k] >= 0;
+        for (int k = 0; k < 4; ++k) rk.band[k] = rk.has[k] || bands_ok(K);
+        rk.pack = side_mask != 0;
+        return rk;
+    };
 
     int cur = 0;  // index of the buffer holding the current state
     auto bufp = [&](int i) { return i ? buf1 : buf0; };
 
+    hipEvent_t ev_edge, ev_int;
+    SMI_TRY(comm_event(c, 0, &ev_edge));
+    SMI_TRY(comm_event(c, 1, &ev_int));
+
     if (side_mask == 0) {  // single tile: no halos, no exchange
-        for (int p = 0; p < kpasses; ++p, cur ^= 1) {
-            ak.in = bufp(cur);
-            ak.out = bufp(cur ^ 1);
-            SMI_TRY(launch_sweepk(K, ak, s));
-        }
-        for (int p = 0; p < pairs; ++p, cur ^= 1) {
-            a2.in = bufp(cur);
-            a2.out = bufp(cur ^ 1);
-            SMI_TRY(launch_sweep2(a2, s));
-        }
-        for (int t = 0; t < singles; ++t, cur ^= 1) {
-            a.in = bufp(cur);
-            a.out = bufp(cur ^ 1);
-            SMI_TRY(launch_sweep(a, s));
+        for (int ph = 0; ph < plan.nph; ++ph) {
+            const int K = plan.k[ph];
+            if (K >= SWEEPK_MIN && bands_ok(K)) {
+                // global-edge bands (comm stream, high priority: dispatched
+                // first) beside the interior sweep, joined every pass
+                SweepKArgs ak = interior_args(K);
+                RingKArgs rk = ring_args(K);
+                SMI_HIP_CHECK(hipEventRecord(ev_int, s));
+                SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
+                for (int p = 0; p < plan.n[ph]; ++p, cur ^= 1) {
+                    rk.in = ak.in = bufp(cur);
+                    rk.out = ak.out = bufp(cur ^ 1);
+                    SMI_TRY(launch_ringk(rk, cs));
+                    SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
+                    SMI_TRY(launch_sweepk(K, ak, s));
+                    SMI_HIP_CHECK(hipEventRecord(ev_int, s));
+                    SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
+                    SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
+                }
+                continue;
+            }
+            SweepKArgs ak = interior_args(K);
+            for (int p = 0; p < plan.n[ph]; ++p, cur ^= 1) {
+                if (K >= SWEEPK_MIN) {
+                    ak.in = bufp(cur);
+                    ak.out = bufp(cur ^ 1);
+                    SMI_TRY(launch_sweepk(K, ak, s));
+                } else if (K == 2) {
+                    a2.in = bufp(cur);
+                    a2.out = bufp(cur ^ 1);
+                    SMI_TRY(launch_sweep2(a2, s));
+                } else {
+                    a.in = bufp(cur);
+                    a.out = bufp(cur ^ 1);
+                    SMI_TRY(launch_sweep(a, s));
+                }
+            }
         }
         return SMI_SUCCESS;
     }
 
     // Halo staging.  Depth 2 (its inner row/column doubles as the depth-1
     // halo): top2 | bot2 | left2 | right2 | corner(4) | send_left2 |
-    // send_right2 | send_corner(4); then depth K: top | bot (K x cols) |
-    // left | right | send_left | send_right (rows x K) | 4 + 4 K x K corners.
+    // send_right2 | send_corner(4); then depth K: top | bot (K x cols) | left
+    // | right | send_left | send_right (rows x K, [row][k]) | 4 + 4 K x K
+    // corners.  The regions are sized for the deepest phase; a shallower
+    // phase (the remainder pass) lays its depth out densely from the start
+    // of each region.
     const size_t need2 = 4 * (size_t)cols + 8 * (size_t)rows + 8;
-    const size_t needk = K ? 2 * (size_t)K * cols + 4 * (size_t)rows * K + 8 * (size_t)K * K : 0;
+    const size_t needk =
+        kmax ? 2 * (size_t)kmax * cols + 4 * (size_t)rows * kmax + 8 * (size_t)kmax * kmax : 0;
     SMI_TRY(ensure_halo(c, need2 + needk));
     Halo2Buf hb;
     hb.top2 = c->halo;
@@ -318,22 +440,22 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     hb.send_right2 = hb.send_left2 + 2 * (size_t)rows;
     hb.send_corner = hb.send_right2 + 2 * (size_t)rows;
     const Halo2 h2 = hb.view();
-    HaloKBuf hk{};
-    if (K) {
+    auto halok = [&]() {
+        HaloKBuf hk{};
         float *p = c->halo + need2;
         hk.top = p;
-        hk.bot = hk.top + (size_t)K * cols;
-        hk.left = hk.bot + (size_t)K * cols;
-        hk.right = hk.left + (size_t)rows * K;
-        hk.send_left = hk.right + (size_t)rows * K;
-        hk.send_right = hk.send_left + (size_t)rows * K;
-        float *q = hk.send_right + (size_t)rows * K;
+        hk.bot = hk.top + (size_t)kmax * cols;
+        hk.left = hk.bot + (size_t)kmax * cols;
+        hk.right = hk.left + (size_t)rows * kmax;
+        hk.send_left = hk.right + (size_t)rows * kmax;
+        hk.send_right = hk.send_left + (size_t)rows * kmax;
+        float *q = hk.send_right + (size_t)rows * kmax;
         for (int k = 0; k < 4; ++k) {
-            hk.corner[k] = q + (size_t)k * K * K;
-            hk.send_corner[k] = q + (size_t)(4 + k) * K * K;
+            hk.corner[k] = q + (size_t)k * kmax * kmax;
+            hk.send_corner[k] = q + (size_t)(4 + k) * kmax * kmax;
         }
-    }
-    const HaloK hkv = hk.view();
+        return hk;
+    };
     // depth-1 views: row -1, row X, col -1, col Y; packed depth-1 sends
     a.halo[0] = hb.top2 + cols;
     a.halo[1] = hb.bot2;
@@ -348,19 +470,6 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
                          const_cast<float *>(a.halo[2]), const_cast<float *>(a.halo[3]), s_left, s_right, st);
     };
     auto xchg2 = [&](const float *tile, hipStream_t st) { return exchange2(c, nb, tile, rows, cols, hb, st); };
-    auto xchgk = [&](const float *tile, hipStream_t st) { return exchangek(c, nb, tile, rows, cols, K, hk, st); };
-    RingKArgs rk{};
-    rk.rows = rows;
-    rk.cols = cols;
-    rk.k = K;
-    for (int k = 0; k < 4; ++k) rk.has[k] = side_nb[k] >= 0;
-    const int diag_nb[4] = {nb.tl, nb.tr, nb.bl, nb.br};
-    for (int k = 0; k < 4; ++k) rk.has_diag[k] = diag_nb[k] >= 0;
-    rk.h = hkv;
-
-    hipEvent_t ev_edge, ev_int;
-    SMI_TRY(comm_event(c, 0, &ev_edge));
-    SMI_TRY(comm_event(c, 1, &ev_int));
 
     // Schedule (two streams, no host synchronisation between passes):
     //   comm stream : [wait interior(t-1)] ring(t) -> rec E_edge(t) -> exchange(t)
@@ -369,9 +478,10 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     // halo-facing cells from its own predecessor) and the halos of
     // exchange(t-1); the interior reads only in(t), never a halo vector, so
     // neither the halo-facing cells nor the xGMI exchange sit on its path.
-    // Each phase (K-step passes, pairs, singles) starts from halos of the
-    // current state: the neighbours' current edges (for the first phase the
-    // reference's artificial timestep t=0, stencil_smi.cl:26-29,183-224).
+    // Each phase (K-step passes, the remainder pass, pairs, singles) starts
+    // from halos of the current state: the neighbours' current edges (for
+    // the first phase the reference's artificial timestep t=0,
+    // stencil_smi.cl:26-29,183-224).
     const bool overlap = g_tune.overlap != 0;
     auto phase_start = [&]() -> int {
         SMI_HIP_CHECK(hipEventRecord(ev_int, s));
@@ -405,51 +515,59 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
         return SMI_SUCCESS;
     };
 
-    // ---- K steps per pass (depth-K halos)
-    if (kpasses > 0) {
+    for (int ph = 0; ph < plan.nph; ++ph) {
+        const int K = plan.k[ph], npass = plan.n[ph];
         SMI_TRY(phase_start());
-        SMI_TRY(launch_packk(bufp(cur), rows, cols, K, hkv, cs));
-        SMI_TRY(xchgk(bufp(cur), cs));
-        for (int p = 0; p < kpasses; ++p, cur ^= 1) {
-            rk.in = ak.in = bufp(cur);
-            rk.out = ak.out = bufp(cur ^ 1);
-            SMI_TRY(pass([&](hipStream_t st) { return launch_ringk(rk, st); },
-                         [&](hipStream_t st) { return launch_sweepk(K, ak, st); }, xchgk, p < kpasses - 1,
-                         ak.out));
-        }
-    }
-    // ---- pairs of steps (depth-2 halos)
-    if (pairs > 0) {
-        SMI_TRY(phase_start());
-        SMI_TRY(launch_pack2(bufp(cur), rows, cols, h2, cs));
-        SMI_TRY(xchg2(bufp(cur), cs));
-        for (int p = 0; p < pairs; ++p, cur ^= 1) {
-            a2.in = bufp(cur);
-            a2.out = bufp(cur ^ 1);
-            SMI_TRY(pass([&](hipStream_t st) { return launch_ring2(a2, h2, st); },
-                         [&](hipStream_t st) { return launch_sweep2(a2, st); }, xchg2, p < pairs - 1, a2.out));
-        }
-    }
-    // ---- single steps (depth-1 halos)
-    if (singles > 0) {
-        SMI_TRY(phase_start());
-        SMI_TRY(launch_pack_cols(bufp(cur), rows, cols, a.send_left, a.send_right, cs));
-        SMI_TRY(xchg1(bufp(cur), cs));
-        SweepArgs inner = a;  // interior launch: halo-facing sides left to the edge kernel
-        for (int k = 0; k < 4; ++k)
-            if (inner.mode[k] == SMI_SIDE_HALO) inner.mode[k] = SMI_SIDE_SKIP;
-        inner.send_left = inner.send_right = nullptr;
-        for (int t = 0; t < singles; ++t, cur ^= 1) {
-            a.in = inner.in = bufp(cur);
-            a.out = inner.out = bufp(cur ^ 1);
-            if (overlap) {
-                SMI_TRY(pass([&](hipStream_t st) { return launch_edge(a, side_mask, st); },
-                             [&](hipStream_t st) { return launch_sweep(inner, st); }, xchg1, t < singles - 1,
-                             a.out));
-            } else {
-                // the full sweep reads the halos itself
-                SMI_TRY(pass([&](hipStream_t) { return (int)SMI_SUCCESS; },
-                             [&](hipStream_t st) { return launch_sweep(a, st); }, xchg1, t < singles - 1, a.out));
+        if (K >= SWEEPK_MIN) {
+            // ---- K steps per pass (depth-K halos)
+            const HaloKBuf hk = halok();
+            const HaloK hkv = hk.view();
+            SweepKArgs ak = interior_args(K);
+            RingKArgs rk = ring_args(K);
+            rk.h = hkv;
+            auto xchgk = [&](const float *tile, hipStream_t st) {
+                return exchangek(c, nb, tile, rows, cols, K, hk, st);
+            };
+            SMI_TRY(launch_packk(bufp(cur), rows, cols, K, hkv, cs));
+            SMI_TRY(xchgk(bufp(cur), cs));
+            for (int p = 0; p < npass; ++p, cur ^= 1) {
+                rk.in = ak.in = bufp(cur);
+                rk.out = ak.out = bufp(cur ^ 1);
+                SMI_TRY(pass([&](hipStream_t st) { return launch_ringk(rk, st); },
+                             [&](hipStream_t st) { return launch_sweepk(K, ak, st); }, xchgk, p < npass - 1,
+                             ak.out));
+            }
+        } else if (K == 2) {
+            // ---- pairs of steps (depth-2 halos)
+            SMI_TRY(launch_pack2(bufp(cur), rows, cols, h2, cs));
+            SMI_TRY(xchg2(bufp(cur), cs));
+            for (int p = 0; p < npass; ++p, cur ^= 1) {
+                a2.in = bufp(cur);
+                a2.out = bufp(cur ^ 1);
+                SMI_TRY(pass([&](hipStream_t st) { return launch_ring2(a2, h2, st); },
+                             [&](hipStream_t st) { return launch_sweep2(a2, st); }, xchg2, p < npass - 1, a2.out));
+            }
+        } else {
+            // ---- single steps (depth-1 halos)
+            SMI_TRY(launch_pack_cols(bufp(cur), rows, cols, a.send_left, a.send_right, cs));
+            SMI_TRY(xchg1(bufp(cur), cs));
+            SweepArgs inner = a;  // interior launch: halo-facing sides left to the edge kernel
+            for (int k = 0; k < 4; ++k)
+                if (inner.mode[k] == SMI_SIDE_HALO) inner.mode[k] = SMI_SIDE_SKIP;
+            inner.send_left = inner.send_right = nullptr;
+            for (int t = 0; t < npass; ++t, cur ^= 1) {
+                a.in = inner.in = bufp(cur);
+                a.out = inner.out = bufp(cur ^ 1);
+                if (overlap) {
+                    SMI_TRY(pass([&](hipStream_t st) { return launch_edge(a, side_mask, st); },
+                                 [&](hipStream_t st) { return launch_sweep(inner, st); }, xchg1, t < npass - 1,
+                                 a.out));
+                } else {
+                    // the full sweep reads the halos itself
+                    SMI_TRY(pass([&](hipStream_t) { return (int)SMI_SUCCESS; },
+                                 [&](hipStream_t st) { return launch_sweep(a, st); }, xchg1, t < npass - 1,
+                                 a.out));
+                }
             }
         }
     }

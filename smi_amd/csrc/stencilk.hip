@@ -1,341 +1,62 @@
-// stencilk.hip -- K Jacobi steps per pass over HBM (deep temporal blocking).
-//
-// Same per-cell arithmetic as every other stencil kernel here
-// (stencil_smi.cl:153-156, global-edge cells copied per :143-151), applied K
-// times inside one streaming pass.  Each wave owns a 256-column window of the
-// input and walks it down a block of rows; every incoming input row advances
-// a pipeline of K levels (level l lags l rows behind the input) and only
-// level K is stored.  The window is 256 input columns wide but stores only
-// the central 256-2K: each level loses one valid column per side, so
-// adjacent windows overlap by 2K columns instead of fetching strip-edge
-// extras (no cross-lane broadcasts).  HBM traffic per pass is that of a
-// single step, so the algorithmic 8 B/cell/step move up to K times faster.
-//
-// Register pipeline.  Level l keeps its last three rows in a 3-slot ring,
-// slot = (input row index) mod 3; the loop body covers 6 input rows (two
-// batches of 3, each batch's loads issued one batch ahead), so every slot
-// index is a compile-time constant and no value is ever moved between
-// registers (a third register batch, loads two batches ahead, measured no
-// faster: profiles/r01f).  The first 2K+1 input rows of a row block prime
-// the pipeline; that prologue is unrolled with compile-time row indices and
-// evaluates level l only from input row 2l on (the rows it must produce).
-// Global-edge copy rules cost nothing in the loop (ROW_* below); only the
-// strips holding column 0 or Y-1 add a per-lane select.
-//
-// The kernel computes an arbitrary output rectangle [row_lo,row_hi) x
-// [col_lo,col_hi) of the tile from input cells within K of it, so it is the
-// single-tile sweep (whole tile) and, in multi-rank runs, the interior sweep
-// that stays K cells clear of every halo-facing side.
-#include <cstdlib>
-#include <type_traits>
-
+// stencilk.hip -- host side of the K-step sweep (kernel: stencilk.h, one
+// instantiation per K in stencilk_k<K>.hip).
 #include "stencil_common.h"
 
 namespace smi {
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+#define SMI_SWEEPK_DECL(K)                                                                           \
+    int sweepk_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, int ht, int blocks, bool full,     \
+                           hipStream_t s);                                                             \
+    int sweepk_resident_k##K();
+SMI_SWEEPK_DECL(3)
+SMI_SWEEPK_DECL(4)
+SMI_SWEEPK_DECL(5)
+SMI_SWEEPK_DECL(6)
+SMI_SWEEPK_DECL(7)
+SMI_SWEEPK_DECL(8)
+SMI_SWEEPK_DECL(9)
+SMI_SWEEPK_DECL(10)
+SMI_SWEEPK_DECL(11)
+SMI_SWEEPK_DECL(12)
 
-// lane i <- lane i-1 / i+1 (DPP wave_shr:1 / wave_shl:1).  Lanes 0 / 63 get
-// whatever the hardware leaves (they only ever feed non-stored columns), so
-// the destination needs no initialisation.
-__device__ __forceinline__ float shr1_any(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
-}
-__device__ __forceinline__ float shl1_any(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
-}
-
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for_from(F &f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for_from<I + 1, N>(f);
-    }
-}
-// f(integral_constant<0>) ... f(integral_constant<N-1>), fully unrolled
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F &&f) {
-    static_for_from<0, N>(f);
-}
-
-// How a wave treats the global edge rows (stencil_smi.cl:143-151: rows 0 and
-// X-1 are copied unchanged every step).
-//   ROW_NONE  the wave's cone never reaches an edge row: no selects at all.
-//   ROW_TOP   the wave's first output row is row 0 (walk downwards).  Row 0
-//             of level l is produced at input t = K + l <= 2K, i.e. only in
-//             the compile-time prologue, so the copy is a handful of
-//             constant-index register moves there -- nothing in the loop.
-//   ROW_BOT   the wave's last output row is row X-1: the wave walks UPWARDS
-//             (N and S swap roles in the loads, never in the arithmetic
-//             order), so row X-1 is again its prologue row t - l = K.
-//   ROW_FULL  anything else that touches an edge row (blocks spanning both
-//             edges, tiny row blocks from a tuning override): per-cell
-//             row selects as before.
-// Column edges add one per-lane select per level step: CE bit 0 for the
-// strip holding column 0, bit 1 for the one holding column Y-1 (both only
-// when one window spans the whole tile); every other wave runs the plain
-// 12-instruction step.
-enum { ROW_NONE = 0, ROW_TOP = 1, ROW_BOT = 2, ROW_FULL = 3 };
-
-template <int K, int U, bool NT>
-struct SweepK {
-    static_assert(K % 4 == 0 && K >= 4 && K <= 12, "K must be a multiple of 4 (float4 lanes)");
-    static_assert(U % 3 == 0, "batch must be a multiple of the 3-slot ring");
-    static constexpr int LL = K / 4;      // lanes per side that never store
-    static constexpr int PRO = 2 * K + 1; // prologue input rows (the last one stores the first output row)
-
-    const float *__restrict__ in;
-    float *__restrict__ out;
-    int rows, cols;
-    int o0, o1;       // output rows of this wave
-    int r_begin;      // input row of t = 0 (o0 - K walking down, o1 - 1 + K walking up)
-    int cl, cb;       // clamped load column / first column of this lane
-    int voff;         // store byte offset in the row (out of range: no store)
-    int row_bytes;
-    bool st, copyL, copyR, gT, gB;
-    float4 W[K][3];   // level 0..K-1, slot = input row index mod 3
-
-    template <bool REV>
-    __device__ __forceinline__ float4 ld(int t) const {
-        const int r = min(max(REV ? r_begin - t : r_begin + t, 0), rows - 1);
-        return *reinterpret_cast<const float4 *>(in + (size_t)r * cols + cl);
-    }
-
-    template <int ROW, int CE>
-    __device__ __forceinline__ float4 step(int i, const float4 &n, const float4 &c, const float4 &s) const {
-        const float w = shr1_any(c.w);
-        const float e = shl1_any(c.x);
-        // ((S + W) + E) element-wise, then (+ N) and (x 0.25) on packed
-        // pairs (v_pk_add_f32 / v_pk_mul_f32: same IEEE single-precision
-        // round-to-nearest results as the scalar ops, never contracted)
-        f32x2 sw01 = {__fadd_rn(s.x, w), __fadd_rn(s.y, c.x)};
-        f32x2 sw23 = {__fadd_rn(s.z, c.y), __fadd_rn(s.w, c.z)};
-        f32x2 swe01 = {__fadd_rn(sw01.x, c.y), __fadd_rn(sw01.y, c.z)};
-        f32x2 swe23 = {__fadd_rn(sw23.x, c.w), __fadd_rn(sw23.y, e)};
-        const f32x2 q = {0.25f, 0.25f};
-        const f32x2 o01 = (swe01 + f32x2{n.x, n.y}) * q;
-        const f32x2 o23 = (swe23 + f32x2{n.z, n.w}) * q;
-        float4 o;
-        o.x = o01.x;
-        o.y = o01.y;
-        o.z = o23.x;
-        o.w = o23.y;
-        if constexpr (ROW == ROW_FULL) {
-            const bool rcopy = (i == 0 && gT) || (i == rows - 1 && gB);
-            o.x = (rcopy || copyL) ? c.x : o.x;
-            o.y = rcopy ? c.y : o.y;
-            o.z = rcopy ? c.z : o.z;
-            o.w = (rcopy || copyR) ? c.w : o.w;
-        } else {
-            if constexpr (CE & 1) o.x = copyL ? c.x : o.x;
-            if constexpr (CE & 2) o.w = copyR ? c.w : o.w;
-        }
-        return o;
-    }
-
-    // level l (1..K) at input t from the level l-1 rows of inputs t-2, t-1, t
-    // (slots PH+1, PH+2, PH mod 3).  Walking down, input t-2 is the upper
-    // row (N) and input t the lower (S); walking up they swap.
-    template <int ROW, int CE, int PH>
-    __device__ __forceinline__ float4 level(int l, int t, const float4 (&P)[3]) const {
-        if constexpr (ROW == ROW_BOT)
-            return step<ROW, CE>(r_begin - (t - l), P[PH], P[(PH + 2) % 3], P[(PH + 1) % 3]);
-        else
-            return step<ROW, CE>(r_begin + t - l, P[(PH + 1) % 3], P[(PH + 2) % 3], P[PH]);
-    }
-
-    // Input row t arrives with value x; PH = t mod 3.
-    template <int ROW, int CE, int PH>
-    __device__ __forceinline__ void advance(int t, const float4 &x) {
-        W[0][PH] = x;
-        float4 v;
-        static_for<K>([&](auto L) {
-            constexpr int l = L + 1;
-            v = level<ROW, CE, PH>(l, t, W[l - 1]);
-            if constexpr (l < K) W[l][PH] = v;
-        });
-        store_row<ROW == ROW_BOT>(t, v);
-    }
-
-    // Branch-free predicated store of the level-K row produced by input t:
-    // a buffer store through a per-row descriptor whose record count is the
-    // row's bytes (0 for rows outside [o0, o1)); lanes that must not store
-    // carry an offset beyond it and the hardware range check drops them.  No
-    // branch splits the unrolled rows, so the scheduler interleaves their
-    // dependency chains.
-    template <bool REV>
-    __device__ __forceinline__ void store_row(int t, const float4 &v) const {
-        const int j = REV ? o1 - 1 - (t - 2 * K) : o0 + (t - 2 * K);
-        const bool in_block = REV ? j >= o0 : j < o1;
-        const int jj = __builtin_amdgcn_readfirstlane(min(max(j, 0), rows - 1));
-        const int nrec = __builtin_amdgcn_readfirstlane(in_block ? row_bytes : 0);
-        __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(out + (size_t)jj * cols, (short)0, nrec, 0x00020000);
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 d = {__builtin_bit_cast(unsigned int, v.x), __builtin_bit_cast(unsigned int, v.y),
-                         __builtin_bit_cast(unsigned int, v.z), __builtin_bit_cast(unsigned int, v.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(d, rs, voff, 0, NT ? 2 : 0);
-    }
-
-    template <int ROW, int CE>
-    __device__ __forceinline__ void run() {
-        constexpr bool REV = ROW == ROW_BOT;
-        // prologue: input rows 0 .. 2K, compile-time indices; level l starts
-        // at input 2l (the first row it must produce)
-        static_for<PRO>([&](auto T) {
-            constexpr int t = T;
-            W[0][t % 3] = ld<REV>(t);
-            float4 v;
-            static_for<K>([&](auto L) {
-                constexpr int l = L + 1;
-                if constexpr (t >= 2 * l) {
-                    v = level<ROW, CE, t % 3>(l, t, W[l - 1]);
-                    // the edge row (0 walking down, X-1 walking up) is input t - l == K
-                    if constexpr ((ROW == ROW_TOP || ROW == ROW_BOT) && t - l == K) v = W[l - 1][(t + 2) % 3];
-                    if constexpr (l < K) W[l][t % 3] = v;
-                }
-            });
-            if constexpr (t == 2 * K) store_row<REV>(t, v);
-        });
-        // steady state: 2U input rows per iteration, loads one batch ahead
-        const int n_in = (o1 - o0) + 2 * K;
-        float4 A[U], B[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) A[u] = ld<REV>(PRO + u);
-        for (int t = PRO; t < n_in; t += 2 * U) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) B[u] = ld<REV>(t + U + u);
-            static_for<U>([&](auto V) {
-                constexpr int ph = (PRO + V) % 3;
-                advance<ROW, CE, ph>(t + V, A[V]);
-            });
-            if (t + U >= n_in) break;  // uniform
-#pragma unroll
-            for (int u = 0; u < U; ++u) A[u] = ld<REV>(t + 2 * U + u);
-            static_for<U>([&](auto V) {
-                constexpr int ph = (PRO + U + V) % 3;
-                advance<ROW, CE, ph>(t + U + V, B[V]);
-            });
-        }
-    }
-};
-
-#ifdef SMI_LOOPBACK_REHEARSAL
-// rehearsal build only (timing experiments): 0 = normal, 1 = every wave runs
-// the global-edge variant, 2 = none does (results then wrong at the edges)
-__device__ int g_edge_force;
+#ifndef SMI_SWEEPK_D
+#define SMI_SWEEPK_D 6
 #endif
 
-template <int K, int U, bool NT>
-__global__ __launch_bounds__(256) void sweepk_kernel(const float *__restrict__ in, float *__restrict__ out,
-                                                     SweepKArgs a, int nstrips, int nrb, int ht) {
-    constexpr int SW = 256 - 2 * K;  // output columns per window
-    const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int lane = threadIdx.x & 63;
-    const int task = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
-    const int rb = task / nstrips;
-    const int strip = task - rb * nstrips;
-    if (rb >= nrb) return;  // wave-uniform
-
-    SweepK<K, U, NT> w;
-    w.in = in;
-    w.out = out;
-    w.rows = a.rows;
-    w.cols = a.cols;
-    // balanced row blocks: every block of a tall rectangle has >= ht/2 rows
-    const int out_rows = a.row_hi - a.row_lo;
-    w.o0 = a.row_lo + (int)((long)rb * out_rows / nrb);
-    w.o1 = a.row_lo + (int)((long)(rb + 1) * out_rows / nrb);
-    const int cs = a.col_lo + strip * SW;
-    w.cb = cs - K + 4 * lane;
-    w.cl = min(max(w.cb, 0), a.cols - 4);
-    w.st = lane >= SweepK<K, U, NT>::LL && lane < 64 - SweepK<K, U, NT>::LL && w.cb < a.col_hi;
-    w.row_bytes = a.cols * 4;
-    w.voff = w.st ? w.cb * 4 : 0x7ffffff0;
-    w.copyL = a.gL && w.cb == 0;
-    w.copyR = a.gR && w.cb + 4 == a.cols;
-    w.gT = a.gT;
-    w.gB = a.gB;
-    // rows any level touches: [o0 - 2K, o1 + K + 5); columns: [cs - K, cs - K + 256)
-    const bool touchT = a.gT && w.o0 - 2 * K <= 0;
-    const bool touchB = a.gB && w.o1 + K + 6 >= a.rows;
-    int ce = ((a.gL && cs - K <= 0) ? 1 : 0) | ((a.gR && cs - K + 256 >= a.cols) ? 2 : 0);
-    int row = ROW_NONE;
-    if (touchT && !touchB && w.o0 == 0)
-        row = ROW_TOP;
-    else if (touchB && !touchT && w.o1 == a.rows)
-        row = ROW_BOT;
-    else if (touchT || touchB)
-        row = ROW_FULL;
-#ifdef SMI_LOOPBACK_REHEARSAL
-    if (g_edge_force == 1) row = ROW_FULL;
-    if (g_edge_force == 2) row = ROW_NONE, ce = 0;
-#endif
-    w.r_begin = row == ROW_BOT ? w.o1 - 1 + K : w.o0 - K;
-    switch (row * 4 + ce) {
-    case 0: w.template run<ROW_NONE, 0>(); break;
-    case 1: w.template run<ROW_NONE, 1>(); break;
-    case 2: w.template run<ROW_NONE, 2>(); break;
-    case 3: w.template run<ROW_NONE, 3>(); break;
-    case 4: w.template run<ROW_TOP, 0>(); break;
-    case 5: w.template run<ROW_TOP, 1>(); break;
-    case 6: w.template run<ROW_TOP, 2>(); break;
-    case 7: w.template run<ROW_TOP, 3>(); break;
-    case 8: w.template run<ROW_BOT, 0>(); break;
-    case 9: w.template run<ROW_BOT, 1>(); break;
-    case 10: w.template run<ROW_BOT, 2>(); break;
-    case 11: w.template run<ROW_BOT, 3>(); break;
-    default: w.template run<ROW_FULL, 3>(); break;
+static int resident_waves(int K) {
+    switch (K) {
+    case 3: return sweepk_resident_k3();
+    case 4: return sweepk_resident_k4();
+    case 5: return sweepk_resident_k5();
+    case 6: return sweepk_resident_k6();
+    case 7: return sweepk_resident_k7();
+    case 8: return sweepk_resident_k8();
+    case 9: return sweepk_resident_k9();
+    case 10: return sweepk_resident_k10();
+    case 11: return sweepk_resident_k11();
+    default: return sweepk_resident_k12();
     }
 }
 
-template <int K, int U>
-static void launch_k(const SweepKArgs &a, int nstrips, int nrb, int ht, int blocks, bool nt, hipStream_t s) {
-    if (nt)
-        hipLaunchKernelGGL((sweepk_kernel<K, U, true>), dim3(blocks), dim3(256), 0, s, a.in, a.out, a, nstrips,
-                           nrb, ht);
-    else
-        hipLaunchKernelGGL((sweepk_kernel<K, U, false>), dim3(blocks), dim3(256), 0, s, a.in, a.out, a, nstrips,
-                           nrb, ht);
-}
-
-// resident waves of sweepk<K> on this device (one round of the grid)
-template <int K, int U>
-static int resident_waves() {
-    static int cached[64] = {};  // per device
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (cached[dev]) return cached[dev];
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweepk_kernel<K, U, true>, 256, 0) != hipSuccess)
-        return 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    cached[dev] = per_cu * cus * 4;
-    return cached[dev];
-}
+int sweepk_window_cols(int K) { return 256 - 8 * ((K + 3) / 4); }
 
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
     if (a.row_hi <= a.row_lo || a.col_hi <= a.col_lo) return SMI_SUCCESS;
-    SMI_ARG_CHECK(K == 4 || K == 8 || K == 12, "sweepk: steps per pass must be 4, 8 or 12");
+    SMI_ARG_CHECK(K >= SWEEPK_MIN && K <= SWEEPK_MAX, "sweepk: steps per pass must be 3..12");
     SMI_ARG_CHECK(a.cols % 4 == 0 && a.col_lo % 4 == 0 && a.col_hi % 4 == 0, "sweepk: columns not float4 aligned");
     SMI_ARG_CHECK(a.row_lo >= 0 && a.row_hi <= a.rows && a.col_lo >= 0 && a.col_hi <= a.cols,
                   "sweepk: output rectangle outside the tile");
-    const int sw = 256 - 2 * K;
+    const int sw = sweepk_window_cols(K);
     const int nstrips = (a.col_hi - a.col_lo + sw - 1) / sw;
     const int out_rows = a.row_hi - a.row_lo;
     int ht = g_tune.htk;
     if (ht <= 0) {
-        // auto: one round of resident waves, each a tall row block of its strip
-        int waves = 0;
-        switch (K) {
-        case 4: waves = resident_waves<4, 3>(); break;
-        case 8: waves = resident_waves<8, 3>(); break;
-        default: waves = resident_waves<12, 3>(); break;
-        }
-        // Single tile: one round of resident waves.  Multi-rank interior:
-        // several rounds, so that workgroups retire during the pass and the
-        // high-priority ring kernel and RCCL exchange on the comm stream are
-        // dispatched then, instead of waiting for the whole interior pass.
+        // auto: one round of resident waves, each a tall row block of its
+        // strip.  Multi-rank interior: several rounds, so that workgroups
+        // retire during the pass and the high-priority ring kernel and RCCL
+        // exchange on the comm stream are dispatched then, instead of waiting
+        // for the whole interior pass.
+        const int waves = resident_waves(K);
         const bool single = a.gT && a.gB && a.gL && a.gR;
         int rounds_multi = g_tune.rounds_multi;
 #ifdef SMI_LOOPBACK_REHEARSAL
@@ -344,30 +65,36 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
         const int rounds = single ? 1 : std::max(1, rounds_multi);
         const int per_strip = std::max(1, waves * rounds / nstrips);
         ht = std::max(2 * K, (out_rows + per_strip - 1) / per_strip);
+        // the steady-state loop advances D+3 rows per iteration with no
+        // per-row guard: heights of 1 mod (D+3) leave no idle rows
+        const int r0 = SMI_SWEEPK_D + 3;
+        ht = 1 + ((ht - 1 + r0 - 1) / r0) * r0;
     }
     const int nrb = (out_rows + ht - 1) / ht;
+    // a stored cell whose cone meets a global edge row or column (its copy
+    // rule) sends the pass to the FULL kernel
+    bool full = (a.gL && a.col_lo < K) || (a.gR && a.col_hi > a.cols - K);
+    for (int rb = 0; rb < nrb && !full; ++rb)
+        full = sweepk_row_class(a, K, a.row_lo + rb * ht, std::min(a.row_lo + (rb + 1) * ht, a.row_hi)) != 0;
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
-#ifdef SMI_LOOPBACK_REHEARSAL
-    {
-        static int cur = 0;
-        const char *e = getenv("SMI_EDGE_FORCE");
-        const int want = e ? atoi(e) : 0;
-        if (want != cur) {
-            SMI_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_edge_force), &want, sizeof(int)));
-            cur = want;
-        }
-    }
-#endif
     int tok = -1;
-    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok));
-    const bool nt = g_tune.nt;
+    if (prof_enabled())
+        SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K));
+    int rc = SMI_SUCCESS;
     switch (K) {
-    case 4: launch_k<4, 3>(a, nstrips, nrb, ht, blocks, nt, s); break;
-    case 8: launch_k<8, 3>(a, nstrips, nrb, ht, blocks, nt, s); break;
-    default: launch_k<12, 3>(a, nstrips, nrb, ht, blocks, nt, s); break;
+    case 3: rc = sweepk_launch_k3(a, nstrips, nrb, ht, blocks, full, s); break;
+    case 4: rc = sweepk_launch_k4(a, nstrips, nrb, ht, blocks, full, s); break;
+    case 5: rc = sweepk_launch_k5(a, nstrips, nrb, ht, blocks, full, s); break;
+    case 6: rc = sweepk_launch_k6(a, nstrips, nrb, ht, blocks, full, s); break;
+    case 7: rc = sweepk_launch_k7(a, nstrips, nrb, ht, blocks, full, s); break;
+    case 8: rc = sweepk_launch_k8(a, nstrips, nrb, ht, blocks, full, s); break;
+    case 9: rc = sweepk_launch_k9(a, nstrips, nrb, ht, blocks, full, s); break;
+    case 10: rc = sweepk_launch_k10(a, nstrips, nrb, ht, blocks, full, s); break;
+    case 11: rc = sweepk_launch_k11(a, nstrips, nrb, ht, blocks, full, s); break;
+    default: rc = sweepk_launch_k12(a, nstrips, nrb, ht, blocks, full, s); break;
     }
-    SMI_HIP_CHECK(hipGetLastError());
+    SMI_TRY(rc);
     if (tok >= 0) SMI_TRY(prof_end(tok, s));
     return SMI_SUCCESS;
 }

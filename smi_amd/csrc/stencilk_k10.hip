@@ -1,0 +1,3 @@
+// stencilk_k10.hip -- sweepk_kernel<10> (see stencilk.h)
+#include "stencilk.h"
+SMI_SWEEPK_INSTANCE(10)

@@ -1,0 +1,3 @@
+// stencilk_k11.hip -- sweepk_kernel<11> (see stencilk.h)
+#include "stencilk.h"
+SMI_SWEEPK_INSTANCE(11)

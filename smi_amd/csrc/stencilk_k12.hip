@@ -1,0 +1,3 @@
+// stencilk_k12.hip -- sweepk_kernel<12> (see stencilk.h)
+#include "stencilk.h"
+SMI_SWEEPK_INSTANCE(12)

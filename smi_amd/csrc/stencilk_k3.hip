@@ -1,0 +1,3 @@
+// stencilk_k3.hip -- sweepk_kernel<3> (see stencilk.h)
+#include "stencilk.h"
+SMI_SWEEPK_INSTANCE(3)

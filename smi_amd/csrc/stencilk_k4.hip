@@ -1,0 +1,3 @@
+// stencilk_k4.hip -- sweepk_kernel<4> (see stencilk.h)
+#include "stencilk.h"
+SMI_SWEEPK_INSTANCE(4)

@@ -1,0 +1,3 @@
+// stencilk_k5.hip -- sweepk_kernel<5> (see stencilk.h)
+#include "stencilk.h"
+SMI_SWEEPK_INSTANCE(5)

@@ -1,0 +1,3 @@
+// stencilk_k6.hip -- sweepk_kernel<6> (see stencilk.h)
+#include "stencilk.h"
+SMI_SWEEPK_INSTANCE(6)

@@ -1,0 +1,3 @@
+// stencilk_k7.hip -- sweepk_kernel<7> (see stencilk.h)
+#include "stencilk.h"
+SMI_SWEEPK_INSTANCE(7)

@@ -1,0 +1,3 @@
+// stencilk_k8.hip -- sweepk_kernel<8> (see stencilk.h)
+#include "stencilk.h"
+SMI_SWEEPK_INSTANCE(8)

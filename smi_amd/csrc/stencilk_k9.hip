@@ -1,0 +1,3 @@
+// stencilk_k9.hip -- sweepk_kernel<9> (see stencilk.h)
+#include "stencilk.h"
+SMI_SWEEPK_INSTANCE(9)

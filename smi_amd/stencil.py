@@ -85,6 +85,25 @@ def run(comm: Comm, tile: torch.Tensor, timesteps: int, PX: int, PY: int,
     return tile if idx.value == 0 else scratch
 
 
+class _Phase(ctypes.Structure):
+    _fields_ = [("steps_per_pass", ctypes.c_int), ("passes", ctypes.c_int)]
+
+
+def plan(x_local: int, y_local: int, PX: int, PY: int, rank: int, timesteps: int) -> dict:
+    """The schedule smi_stencil_run follows on `rank` (host only, no GPU):
+    phases [(steps_per_pass, passes), ...], the neighbour ranks (top, bottom,
+    left, right, tl, tr, bl, br; -1 on the global edge) and the index of the
+    buffer that ends up holding the result."""
+    ph = (_Phase * 4)()
+    n = ctypes.c_int()
+    nb = (ctypes.c_int * 8)()
+    ri = ctypes.c_int()
+    _lib.call("smi_stencil_plan", x_local, y_local, PX, PY, rank, timesteps, ph, 4, ctypes.byref(n), nb,
+              ctypes.byref(ri))
+    return {"phases": [(ph[i].steps_per_pass, ph[i].passes) for i in range(n.value)],
+            "neighbours": list(nb), "result_index": ri.value}
+
+
 def set_tuning(rows_per_wave: int = 0, rows_in_flight: int = 0, nontemporal: int = -1,
                overlap: int = -1) -> None:
     _lib.call("smi_stencil_set_tuning", rows_per_wave, rows_in_flight, nontemporal, overlap)
@@ -98,7 +117,9 @@ def get_tuning() -> dict:
 
 
 def set_fusion(steps_per_pass: int = 0, rows_per_wave: int = 0, rows_in_flight: int = 0) -> None:
-    """1 = one Jacobi step per pass over HBM, 2 = two fused steps (same bits)."""
+    """Up to steps_per_pass (1..12) Jacobi steps fused per pass over HBM
+    (same bits for every setting); the remainder of a run is one shallower
+    pass (smi_stencil_plan)."""
     _lib.call("smi_stencil_set_fusion", steps_per_pass, rows_per_wave, rows_in_flight)
 
 

@@ -1,9 +1,12 @@
 """Host-side logic on CPU: decomposition helpers (SplitMemory/CombineMemory,
-rank map), gesummv row split, bench decomposition, and the world_size=2
-gloo bring-up of the RCCL unique id + a decomposed stencil whose halos move
-through gloo point-to-point (the Convert{Send,Receive}* protocol of
-stencil_smi.cl:236-386 with the same neighbour/port mapping as the C++
-runtime), checked against the single-grid oracle."""
+rank map), the run planner of libsmi_amd (smi_stencil_plan: phases, the
+neighbour map, the result buffer), gesummv row split, bench decomposition,
+and the world_size=2 gloo bring-up of the RCCL unique id + a decomposed
+stencil that follows libsmi_amd's own plan and neighbour map and moves its
+depth-K halos (K rows / columns per side, K x K corner blocks) through gloo
+point-to-point -- the schedule of smi_stencil_run replacing the
+Convert{Send,Receive}* kernels of stencil_smi.cl:236-386 -- checked against
+the single-grid oracle."""
 import os
 import socket
 
@@ -71,6 +74,66 @@ def test_bench_halo_report_counts_neighbours():
     assert h1["neighbours"] == {"vertical": 0, "horizontal": 1, "diagonal": 0}
 
 
+# ------------------------------------------------------------ run planner --
+def test_plan_splits_steps_into_deep_passes_and_one_remainder():
+    """smi_stencil_plan (host only): T // 12 passes of 12 steps, then ONE pass
+    of the remainder r when r >= 3, else a pair and/or a single step."""
+    from smi_amd import stencil
+    for T in range(0, 60):
+        ph = stencil.plan(8192, 8192, 1, 1, 0, T)["phases"]
+        assert sum(k * n for k, n in ph) == T
+        q, r = divmod(T, 12)
+        want = ([(12, q)] if q else []) + ([(r, 1)] if r >= 3 else ([(r, 1)] if r else []))
+        assert ph == want, (T, ph)
+        assert stencil.plan(8192, 8192, 1, 1, 0, T)["result_index"] == sum(n for _, n in ph) % 2
+    assert stencil.plan(8192, 8192, 1, 1, 0, 20)["phases"] == [(12, 1), (8, 1)]  # the driver's --steps 20
+
+
+def test_plan_neighbours_follow_reference_rank_map():
+    """rank = i_px * PY + i_py (stencil_smi.cpp:133-134); diagonals where both
+    sides exist."""
+    from smi_amd import stencil
+    for PX, PY in [(1, 2), (2, 1), (2, 2), (2, 4), (3, 3)]:
+        for r in range(PX * PY):
+            ipx, ipy = divmod(r, PY)
+            nb = stencil.plan(64, 64, PX, PY, r, 5)["neighbours"]
+            at = lambda dx, dy: ((ipx + dx) * PY + ipy + dy  # noqa: E731
+                                 if 0 <= ipx + dx < PX and 0 <= ipy + dy < PY else -1)
+            assert nb == [at(-1, 0), at(1, 0), at(0, -1), at(0, 1), at(-1, -1), at(-1, 1), at(1, -1), at(1, 1)]
+
+
+def test_plan_clips_k_to_the_tile():
+    from smi_amd import stencil
+    assert stencil.plan(10, 16, 2, 2, 0, 23)["phases"] == [(5, 4), (3, 1)]
+    assert stencil.plan(10, 16, 1, 1, 0, 23)["phases"] == [(12, 1), (11, 1)]  # single tile: no halo limit
+    assert stencil.plan(4, 4, 1, 1, 0, 5)["phases"] == [(1, 5)]                # below 4 x 8: single steps
+    assert stencil.plan(4, 8, 2, 2, 0, 5)["phases"] == [(2, 2), (1, 1)]
+
+
+def test_plan_rejects_bad_arguments():
+    from smi_amd import SMIError, stencil
+    with pytest.raises(SMIError):
+        stencil.plan(8, 6, 1, 1, 0, 3)      # y_local % 4
+    with pytest.raises(SMIError):
+        stencil.plan(8, 8, 2, 2, 4, 3)      # rank outside the grid
+    with pytest.raises(SMIError):
+        stencil.plan(8, 8, 1, 1, 0, -1)
+
+
+def test_fusion_setting_drives_the_plan():
+    from smi_amd import stencil
+    old = stencil.get_fusion()
+    try:
+        stencil.set_fusion(8)
+        assert stencil.plan(256, 256, 1, 1, 0, 20)["phases"] == [(8, 2), (4, 1)]
+        stencil.set_fusion(2)
+        assert stencil.plan(256, 256, 1, 1, 0, 7)["phases"] == [(2, 3), (1, 1)]
+        stencil.set_fusion(1)
+        assert stencil.plan(256, 256, 1, 1, 0, 7)["phases"] == [(1, 7)]
+    finally:
+        stencil.set_fusion(old["steps_per_pass"])
+
+
 # ------------------------------------------------------ gloo, world_size 2 --
 def _free_port():
     s = socket.socket()
@@ -80,12 +143,48 @@ def _free_port():
     return p
 
 
-def _neighbours(rank, PX, PY):
-    ipx, ipy = rank // PY, rank % PY
-    return dict(top=(ipx - 1) * PY + ipy if ipx > 0 else -1,
-                bottom=(ipx + 1) * PY + ipy if ipx < PX - 1 else -1,
-                left=rank - 1 if ipy > 0 else -1,
-                right=rank + 1 if ipy < PY - 1 else -1)
+def _exchange_depth(dist, torch, tile, nb, k):
+    """One depth-k exchange with the libsmi_amd neighbour map: k rows to the
+    vertical neighbours, k columns to the horizontal ones, a k x k block to
+    each diagonal one; returns the extended tile (padded only on sides that
+    have a neighbour: global edges stay the grid's own edges)."""
+    X, Y = tile.shape
+    top, bottom, left, right, tl, tr, bl, br = nb
+    parts = [(top, tile[:k]), (bottom, tile[X - k:]), (left, tile[:, :k]), (right, tile[:, Y - k:]),
+             (tl, tile[:k, :k]), (tr, tile[:k, Y - k:]), (bl, tile[X - k:, :k]), (br, tile[X - k:, Y - k:])]
+    reqs, recv = [], []
+    for peer, data in parts:
+        if peer < 0:
+            recv.append(None)
+            continue
+        buf = torch.empty(data.shape)
+        reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(data)), peer))
+        reqs.append(dist.irecv(buf, peer))
+        recv.append(buf)
+    for r in reqs:
+        r.wait()
+    h = [None if b is None else b.numpy() for b in recv]
+    pt, pb, pl, pr = (k if top >= 0 else 0), (k if bottom >= 0 else 0), (k if left >= 0 else 0), \
+        (k if right >= 0 else 0)
+    ext = np.zeros((X + pt + pb, Y + pl + pr), np.float32)
+    ext[pt:pt + X, pl:pl + Y] = tile
+    if h[0] is not None:
+        ext[:pt, pl:pl + Y] = h[0]
+    if h[1] is not None:
+        ext[pt + X:, pl:pl + Y] = h[1]
+    if h[2] is not None:
+        ext[pt:pt + X, :pl] = h[2]
+    if h[3] is not None:
+        ext[pt:pt + X, pl + Y:] = h[3]
+    if h[4] is not None:
+        ext[:pt, :pl] = h[4]
+    if h[5] is not None:
+        ext[:pt, pl + Y:] = h[5]
+    if h[6] is not None:
+        ext[pt + X:, :pl] = h[6]
+    if h[7] is not None:
+        ext[pt + X:, pl + Y:] = h[7]
+    return ext, pt, pl
 
 
 def _worker(rank, world, port, PX, PY, T, q):
@@ -95,70 +194,46 @@ def _worker(rank, world, port, PX, PY, T, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        from smi_amd import stencil
         from smi_amd.comm import exchange_unique_id
         uid = exchange_unique_id(rank, world, dist.distributed_c10d._get_default_store(), key="t/uid")
         ids = [None] * world
         dist.all_gather_object(ids, uid)
-        g = o.init_uniform(16 * PX, 12 * PY, seed=9)
-        XL, YL = 16, 12
+        XL, YL = 24, 28
+        g = o.init_uniform(XL * PX, YL * PY, seed=9)
         ipx, ipy = rank // PY, rank % PY
         tile = g[ipx * XL:(ipx + 1) * XL, ipy * YL:(ipy + 1) * YL].copy()
-        nb = _neighbours(rank, PX, PY)
-        for _ in range(T):
-            ext = np.zeros((XL + 2, YL + 2), np.float32)
-            ext[1:-1, 1:-1] = tile
-            reqs = []
-            bufs = {}
-            for side, peer, data in (("top", nb["top"], tile[0]), ("bottom", nb["bottom"], tile[-1]),
-                                     ("left", nb["left"], tile[:, 0]), ("right", nb["right"], tile[:, -1])):
-                if peer < 0:
-                    continue
-                reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(data)), peer))
-                bufs[side] = torch.empty(len(data))
-                reqs.append(dist.irecv(bufs[side], peer))
-            for r in reqs:
-                r.wait()
-            if "top" in bufs:
-                ext[0, 1:-1] = bufs["top"].numpy()
-            if "bottom" in bufs:
-                ext[-1, 1:-1] = bufs["bottom"].numpy()
-            if "left" in bufs:
-                ext[1:-1, 0] = bufs["left"].numpy()
-            if "right" in bufs:
-                ext[1:-1, -1] = bufs["right"].numpy()
-            new = o.stencil(ext, 1)[1:-1, 1:-1].copy()
-            # global edges are copied (stencil_smi.cl:143-151)
-            if nb["top"] < 0:
-                new[0] = tile[0]
-            if nb["bottom"] < 0:
-                new[-1] = tile[-1]
-            if nb["left"] < 0:
-                new[:, 0] = tile[:, 0]
-            if nb["right"] < 0:
-                new[:, -1] = tile[:, -1]
-            tile = new
+        plan = stencil.plan(XL, YL, PX, PY, rank, T)   # libsmi_amd's own schedule
+        for k, passes in plan["phases"]:
+            for _ in range(passes):
+                ext, pt, pl = _exchange_depth(dist, torch, tile, plan["neighbours"], k)
+                tile = o.stencil(ext, k)[pt:pt + XL, pl:pl + YL].copy()
         tiles = [None] * world
         dist.all_gather_object(tiles, tile)
+        plans = [None] * world
+        dist.all_gather_object(plans, plan["phases"])
         if rank == 0:
-            from smi_amd import stencil
             got = stencil.combine_memory(tiles, PX, PY)
-            q.put((ids[0] == ids[1] and len(ids[0]) == 128,
+            q.put((all(i == ids[0] for i in ids) and len(ids[0]) == 128, all(p == plans[0] for p in plans),
                    bool(np.array_equal(got.view(np.uint32), o.stencil(g, T).view(np.uint32)))))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pxpy", [(1, 2), (2, 1)])
-def test_gloo_world2_halo_protocol(pxpy):
+@pytest.mark.parametrize("pxpy,T", [((1, 2), 29), ((2, 1), 29), ((1, 2), 6), ((2, 2), 27)])
+def test_gloo_world2_halo_protocol(pxpy, T):
+    """world_size 2 (1x2, 2x1) and 4 (2x2: diagonal K x K corner blocks)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, pxpy[0], pxpy[1], 6, q)) for r in range(2)]
+    world = pxpy[0] * pxpy[1]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, pxpy[0], pxpy[1], T, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0
-    same_uid, exact = q.get(timeout=5)
+    same_uid, same_plan, exact = q.get(timeout=5)
     assert same_uid, "RCCL unique id not shared through the store"
-    assert exact, "decomposed halo protocol differs from the single-grid oracle"
+    assert same_plan, "ranks planned different phases"
+    assert exact, "decomposed depth-K halo protocol differs from the single-grid oracle"

@@ -251,8 +251,8 @@ def test_fused_full_size_8192(gpu, oracle_mod):
     assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 4)))
 
 
-# --------------------------------------------- K = 4, 8 steps per pass (deep) --
-@pytest.mark.parametrize("k", [4, 8, 12])
+# ------------------------------------------ K = 3..12 steps per pass (deep) --
+@pytest.mark.parametrize("k", [3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("shape", [(1, 4), (2, 8), (5, 8), (9, 12), (17, 260), (64, 64), (129, 500),
                                    (300, 1028), (1000, 516)])
 def test_deep_single_tile(gpu, oracle_mod, k, shape):
@@ -263,7 +263,7 @@ def test_deep_single_tile(gpu, oracle_mod, k, shape):
         assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, shape, T)
 
 
-@pytest.mark.parametrize("k", [4, 8, 12])
+@pytest.mark.parametrize("k", [3, 4, 7, 8, 12])
 @pytest.mark.parametrize("ht,u", [(1, 2), (5, 4), (16, 8), (32, 2), (100, 8)])
 def test_deep_tuning_is_bit_neutral(gpu, oracle_mod, k, ht, u):
     g = oracle_mod.init_uniform(517, 1540, seed=11)
@@ -283,8 +283,61 @@ def test_deep_full_size_8192(gpu, oracle_mod):
     assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 8)))
 
 
+def test_bench_config_full_size_k12(gpu, oracle_mod):
+    """BASELINE config 2 exactly as bench.py runs it: 8192^2 fp32, the default
+    K = 12 and automatic row blocks, T = 12 (one pass), 20 (12 + 8: the
+    driver's --steps 20) and 25 (12 + 12 + 1), bit-exact vs the oracle."""
+    from smi_amd import LocalGroup, stencil
+    assert stencil.get_fusion()["steps_per_pass"] == 12
+    g = oracle_mod.init_uniform(8192, 8192, seed=1000)
+    comm = LocalGroup(1).comm(0)
+    want = g
+    done = 0
+    for T in (12, 20, 25):
+        want = oracle_mod.stencil(want, T - done)
+        done = T
+        t = torch.from_numpy(g).cuda()
+        res = stencil.run(comm, t, T, 1, 1)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(res.cpu().numpy()), bits(want)), T
+        del t, res
+    comm.finalize()
+
+
+@pytest.mark.parametrize("T", list(range(1, 27)))
+def test_remainder_plan_every_step_count(gpu, oracle_mod, T):
+    """Every step count 1..26 under the default K = 12 (K-step passes, then
+    one remainder pass of 3..11 steps, or a pair / single step)."""
+    from smi_amd import stencil
+    g = oracle_mod.init_uniform(203, 780, seed=T)
+    ph = stencil.plan(203, 780, 1, 1, 0, T)["phases"]
+    assert sum(k * n for k, n in ph) == T
+    assert np.array_equal(bits(_run_fused(g, T, k=12)), bits(oracle_mod.stencil(g, T)))
+
+
+@pytest.mark.parametrize("T", [5, 13, 14, 23, 31])
+@pytest.mark.parametrize("pxpy", [(2, 2), (1, 3)])
+def test_remainder_plan_decomposed(gpu, oracle_mod, T, pxpy):
+    """Multi-rank runs whose plan ends in a remainder pass (depth-r halos from
+    the same staging as depth 12) or a pair / single step."""
+    PX, PY = pxpy
+    g = oracle_mod.init_uniform(48 * PX, 64 * PY, seed=T + PX)
+    for overlap in (0, 1):
+        got = _run_fused(g, T, PX, PY, overlap, k=12)
+        assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (T, pxpy, overlap)
+
+
+def test_clipped_k_on_small_tiles(gpu, oracle_mod):
+    """Tiles smaller than 24 x 24 in a multi-rank run clip K to half the
+    smaller side (here 10 x 16 tiles: K = 5) instead of dropping to pairs."""
+    from smi_amd import stencil
+    assert stencil.plan(10, 16, 2, 2, 0, 23)["phases"] == [(5, 4), (3, 1)]
+    g = oracle_mod.init_uniform(20, 32, seed=5)
+    assert np.array_equal(bits(_run_fused(g, 23, 2, 2, k=12)), bits(oracle_mod.stencil(g, 23)))
+
+
 @pytest.mark.parametrize("overlap", [0, 1])
-@pytest.mark.parametrize("k", [4, 8, 12])
+@pytest.mark.parametrize("k", [3, 4, 8, 12])
 @pytest.mark.parametrize("pxpy", [(2, 1), (1, 2), (2, 2), (2, 4), (3, 3)])
 def test_deep_decomposed(gpu, oracle_mod, k, pxpy, overlap):
     """K-step passes with depth-K halos and K x K corner blocks, then the
@@ -301,7 +354,7 @@ def test_deep_decomposed_small_tiles(gpu, oracle_mod, k):
     # exactly 2K x 2K tiles (smallest deep tile), ring blocks larger than tiles
     g = oracle_mod.init_uniform(4 * k, 6 * k, seed=k)
     assert np.array_equal(bits(_run_fused(g, 3 * k + 1, 2, 3, k=k)), bits(oracle_mod.stencil(g, 3 * k + 1)))
-    # tiles below 2K fall back to pairs/singles
+    # tiles below 2K clip K (or fall back to pairs/singles below 6 x 8)
     g = oracle_mod.init_uniform(2 * k - 4, 4 * k, seed=k + 1)
     assert np.array_equal(bits(_run_fused(g, 2 * k, 2, 2, k=k)), bits(oracle_mod.stencil(g, 2 * k)))
     # config 1 (256^2, 2x2, 32 steps) through the deep path

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-2: LDS-DMA input ring -- parity, tuning (release / no-edge timing experiment / D=9)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r02b
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_stencil_gpu.py -x -q --timeout 300 --timeout-method thread > $O/stencil_tests.log 2>&1 || { echo "stencil tests failed"; tail -30 $O/stencil_tests.log; exit 1; }
+tail -2 $O/stencil_tests.log
+timeout -k 10 200 python -u tools/tune_deep.py 8192 20 12,10,8 -1,100 > $O/tune_release.jsonl 2>&1 || exit 1
+SMI_LIB_VARIANT=exp_noedge timeout -k 10 120 python -u tools/tune_deep.py 8192 20 12,10 -1,73,100 > $O/tune_noedge.jsonl 2>&1 || exit 1
+SMI_LIB_VARIANT=exp_d9 timeout -k 10 120 python -u tools/tune_deep.py 8192 20 12 -1,100 > $O/tune_d9.jsonl 2>&1 || exit 1
+cat $O/tune_*.jsonl | grep -v amdgpu.ids
+timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-aux --no-cpu-baseline > $O/bench_20_5.json 2> $O/bench_20_5.err || exit 1
+python -c "import json;d=json.load(open('$O/bench_20_5.json'));print(d['value'],d['ms_per_step'],[(k['kernel'][:16],k['total_ms']) for k in d['roofline']['kernels']])"
