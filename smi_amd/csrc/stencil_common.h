@@ -76,7 +76,7 @@ struct Tuning {
     // where workgroups retire, so the RCCL kernel of the exchange is never
     // left without a slot until the interior ends.
     int rounds_multi = 2;
-    int uk = 6;         // rows loaded ahead (K-step sweep: fixed at build time, SMI_SWEEPK_D)
+    int uk = 3;         // rows loaded ahead (K-step sweep: one 3-row register batch, fixed at build time)
 };
 extern Tuning g_tune;
 
@@ -120,17 +120,6 @@ struct SweepKArgs {
     int gT, gB, gL, gR;
 };
 constexpr int SWEEPK_MIN = 3, SWEEPK_MAX = 12;
-// How a K-step row block [o0, o1) meets the global edge rows: 0 its cone
-// never reaches one (fast kernel), 1 holds row 0 only, 2 holds row X-1 only,
-// 3 otherwise; anything but 0 takes the FULL kernel (stencilk.h).  The cone
-// spans rows [o0 - K, o1 + K); the margins are generous.
-__host__ __device__ inline int sweepk_row_class(const SweepKArgs &a, int K, int o0, int o1) {
-    const bool touchT = a.gT && o0 - 2 * K <= 0;
-    const bool touchB = a.gB && o1 + K + 6 >= a.rows;
-    if (touchT && !touchB && o0 == 0) return 1;
-    if (touchB && !touchT && o1 == a.rows) return 2;
-    return (touchT || touchB) ? 3 : 0;
-}
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s);
 int sweepk_window_cols(int K);  // output columns per 256-column window
 

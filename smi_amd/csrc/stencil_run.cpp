@@ -333,28 +333,22 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     a2.cols = cols;
     for (int k = 0; k < 4; ++k) a2.skip[k] = side_nb[k] >= 0;
     // K-step passes: the interior sweep stays K rows / 4*ceil(K/4) columns
-    // clear of every halo-facing side AND of the global edges (whose copy
-    // rule stencil_smi.cl:143-151 would cost the fast sweep a wave per SIMD,
-    // stencilk.h); the ring kernel computes those bands beside it.  Tiles too
-    // small for the bands run their global-edge sides through the sweep's
-    // FULL kernel.
+    // clear of every halo-facing side (the ring kernel computes those bands
+    // beside it); global edges are handled inside the sweep (stencilk.h).
     auto kc_of = [](int K) { return 4 * ((K + 3) / 4); };
-    auto bands_ok = [&](int K) { return rows >= 4 * K && cols >= 4 * kc_of(K); };
     auto interior_args = [&](int K) {
         SweepKArgs ak{};
         ak.rows = rows;
         ak.cols = cols;
-        const bool bands = bands_ok(K);
         const int kc = kc_of(K);
-        ak.row_lo = (nb.top >= 0 || bands) ? K : 0;
-        ak.row_hi = (nb.bottom >= 0 || bands) ? rows - K : rows;
-        ak.col_lo = (nb.left >= 0 || bands) ? kc : 0;
-        ak.col_hi = (nb.right >= 0 || bands) ? cols - kc : cols;
-        // a global edge inside the interior's cone only without bands
-        ak.gT = nb.top < 0 && !bands;
-        ak.gB = nb.bottom < 0 && !bands;
-        ak.gL = nb.left < 0 && !bands;
-        ak.gR = nb.right < 0 && !bands;
+        ak.row_lo = nb.top >= 0 ? K : 0;
+        ak.row_hi = nb.bottom >= 0 ? rows - K : rows;
+        ak.col_lo = nb.left >= 0 ? kc : 0;
+        ak.col_hi = nb.right >= 0 ? cols - kc : cols;
+        ak.gT = nb.top < 0;
+        ak.gB = nb.bottom < 0;
+        ak.gL = nb.left < 0;
+        ak.gR = nb.right < 0;
         return ak;
     };
     const int diag_nb[4] = {nb.tl, nb.tr, nb.bl, nb.br};
@@ -365,7 +359,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
         rk.k = K;
         for (int k = 0; k < 4; ++k) rk.has[k] = side_nb[k] >= 0;
         for (int k = 0; k < 4; ++k) rk.has_diag[k] = diag_nb[k] >= 0;
-        for (int k = 0; k < 4; ++k) rk.band[k] = rk.has[k] || bands_ok(K);
+        for (int k = 0; k < 4; ++k) rk.band[k] = rk.has[k];
         rk.pack = side_mask != 0;
         return rk;
     };
@@ -380,25 +374,6 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     if (side_mask == 0) {  // single tile: no halos, no exchange
         for (int ph = 0; ph < plan.nph; ++ph) {
             const int K = plan.k[ph];
-            if (K >= SWEEPK_MIN && bands_ok(K)) {
-                // global-edge bands (comm stream, high priority: dispatched
-                // first) beside the interior sweep, joined every pass
-                SweepKArgs ak = interior_args(K);
-                RingKArgs rk = ring_args(K);
-                SMI_HIP_CHECK(hipEventRecord(ev_int, s));
-                SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
-                for (int p = 0; p < plan.n[ph]; ++p, cur ^= 1) {
-                    rk.in = ak.in = bufp(cur);
-                    rk.out = ak.out = bufp(cur ^ 1);
-                    SMI_TRY(launch_ringk(rk, cs));
-                    SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-                    SMI_TRY(launch_sweepk(K, ak, s));
-                    SMI_HIP_CHECK(hipEventRecord(ev_int, s));
-                    SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-                    SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
-                }
-                continue;
-            }
             SweepKArgs ak = interior_args(K);
             for (int p = 0; p < plan.n[ph]; ++p, cur ^= 1) {
                 if (K >= SWEEPK_MIN) {

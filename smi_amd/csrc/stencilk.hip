@@ -5,8 +5,7 @@
 namespace smi {
 
 #define SMI_SWEEPK_DECL(K)                                                                           \
-    int sweepk_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, int ht, int blocks, bool full,     \
-                           hipStream_t s);                                                             \
+    int sweepk_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s);        \
     int sweepk_resident_k##K();
 SMI_SWEEPK_DECL(3)
 SMI_SWEEPK_DECL(4)
@@ -18,10 +17,6 @@ SMI_SWEEPK_DECL(9)
 SMI_SWEEPK_DECL(10)
 SMI_SWEEPK_DECL(11)
 SMI_SWEEPK_DECL(12)
-
-#ifndef SMI_SWEEPK_D
-#define SMI_SWEEPK_D 6
-#endif
 
 static int resident_waves(int K) {
     switch (K) {
@@ -65,17 +60,8 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
         const int rounds = single ? 1 : std::max(1, rounds_multi);
         const int per_strip = std::max(1, waves * rounds / nstrips);
         ht = std::max(2 * K, (out_rows + per_strip - 1) / per_strip);
-        // the steady-state loop advances D+3 rows per iteration with no
-        // per-row guard: heights of 1 mod (D+3) leave no idle rows
-        const int r0 = SMI_SWEEPK_D + 3;
-        ht = 1 + ((ht - 1 + r0 - 1) / r0) * r0;
     }
     const int nrb = (out_rows + ht - 1) / ht;
-    // a stored cell whose cone meets a global edge row or column (its copy
-    // rule) sends the pass to the FULL kernel
-    bool full = (a.gL && a.col_lo < K) || (a.gR && a.col_hi > a.cols - K);
-    for (int rb = 0; rb < nrb && !full; ++rb)
-        full = sweepk_row_class(a, K, a.row_lo + rb * ht, std::min(a.row_lo + (rb + 1) * ht, a.row_hi)) != 0;
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
     int tok = -1;
@@ -83,16 +69,16 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
         SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K));
     int rc = SMI_SUCCESS;
     switch (K) {
-    case 3: rc = sweepk_launch_k3(a, nstrips, nrb, ht, blocks, full, s); break;
-    case 4: rc = sweepk_launch_k4(a, nstrips, nrb, ht, blocks, full, s); break;
-    case 5: rc = sweepk_launch_k5(a, nstrips, nrb, ht, blocks, full, s); break;
-    case 6: rc = sweepk_launch_k6(a, nstrips, nrb, ht, blocks, full, s); break;
-    case 7: rc = sweepk_launch_k7(a, nstrips, nrb, ht, blocks, full, s); break;
-    case 8: rc = sweepk_launch_k8(a, nstrips, nrb, ht, blocks, full, s); break;
-    case 9: rc = sweepk_launch_k9(a, nstrips, nrb, ht, blocks, full, s); break;
-    case 10: rc = sweepk_launch_k10(a, nstrips, nrb, ht, blocks, full, s); break;
-    case 11: rc = sweepk_launch_k11(a, nstrips, nrb, ht, blocks, full, s); break;
-    default: rc = sweepk_launch_k12(a, nstrips, nrb, ht, blocks, full, s); break;
+    case 3: rc = sweepk_launch_k3(a, nstrips, nrb, blocks, s); break;
+    case 4: rc = sweepk_launch_k4(a, nstrips, nrb, blocks, s); break;
+    case 5: rc = sweepk_launch_k5(a, nstrips, nrb, blocks, s); break;
+    case 6: rc = sweepk_launch_k6(a, nstrips, nrb, blocks, s); break;
+    case 7: rc = sweepk_launch_k7(a, nstrips, nrb, blocks, s); break;
+    case 8: rc = sweepk_launch_k8(a, nstrips, nrb, blocks, s); break;
+    case 9: rc = sweepk_launch_k9(a, nstrips, nrb, blocks, s); break;
+    case 10: rc = sweepk_launch_k10(a, nstrips, nrb, blocks, s); break;
+    case 11: rc = sweepk_launch_k11(a, nstrips, nrb, blocks, s); break;
+    default: rc = sweepk_launch_k12(a, nstrips, nrb, blocks, s); break;
     }
     SMI_TRY(rc);
     if (tok >= 0) SMI_TRY(prof_end(tok, s));
