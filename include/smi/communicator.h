@@ -12,6 +12,24 @@
  * every pair of GPUs is one xGMI hop, so initialisation is just an RCCL
  * communicator (or, for single-GPU testing, an in-process group whose ranks
  * are host threads sharing one device).
+ *
+ * Ordering and threads.  A communicator carries two independent matching
+ * spaces:
+ *   - bulk operations (smi_reduce, smi_bcast, smi_scatter, smi_gather,
+ *     smi_send/smi_recv, smi_gesummv, the stencil exchanges) are matched with
+ *     the other ranks' in issue order per rank pair, as RCCL matches them:
+ *     every rank issues its bulk operations in the same order, from one host
+ *     thread at a time (concurrent callers are serialised per transport
+ *     group, but a second thread's operation would still interleave in the
+ *     issue order and share the communicator's staging workspace).  The
+ *     `port` argument of a bulk call is informational.
+ *   - element-granular channels (SMI_Push/SMI_Pop, SMI_Bcast, SMI_Reduce,
+ *     SMI_Scatter, SMI_Gather) travel on a communicator of their own (an
+ *     RCCL communicator split off at smi_init, pre-connected to every peer),
+ *     tagged by port and demultiplexed into one FIFO per (source, port), like
+ *     the reference's per-port channels: a packet pushed before a collective
+ *     is never consumed by it, and channels on different ports may be driven
+ *     from different host threads.
  */
 #ifndef SMI_COMMUNICATOR_H
 #define SMI_COMMUNICATOR_H

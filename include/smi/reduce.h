@@ -33,9 +33,15 @@ typedef enum {
 } SMI_Op;
 
 /* Reduce `count` elements of every rank's device buffer `sendbuf` into the
- * root's device buffer `recvbuf` (ignored on other ranks).  `port` tags the
- * operation like the reference's logical port (ops on different ports may be
- * issued from different host threads).  Enqueued on `stream`. */
+ * root's device buffer `recvbuf` (ignored on other ranks), enqueued on
+ * `stream`.  `port` is informational: like every bulk operation of a
+ * communicator (include/smi/communicator.h), a reduce is matched with the
+ * other ranks' in issue order, so all ranks issue their bulk operations in
+ * the same order (the reference orders them by port).
+ * Schedule: owner-chunk exchange -> canonical rank-order fold on each owner
+ * -> gather on the root, pipelined over pieces of smi_set_pipeline_bytes()
+ * bytes per owner chunk (the fold of one piece overlaps the exchange of the
+ * next).  Results do not depend on the piece size. */
 int smi_reduce(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count,
                SMI_Datatype type, SMI_Op op, int root, int port,
                SMI_Stream stream);
@@ -51,6 +57,12 @@ SMI_RChannel SMI_Open_reduce_channel(int count, SMI_Datatype data_type, SMI_Op o
 SMI_RChannel SMI_Open_reduce_channel_ad(int count, SMI_Datatype data_type, SMI_Op op, int port, int root,
                                         SMI_Comm comm, int asynch_degree);
 void SMI_Reduce(SMI_RChannel *chan, void *data_snd, void *data_rcv);
+
+/* Piece size (bytes per owner chunk) of the pipelined smi_reduce/smi_bcast;
+ * 0 = one piece per chunk.  Default 4 MiB.  Process-wide; set it between
+ * operations, identically on every rank. */
+int smi_set_pipeline_bytes(size_t piece_bytes);
+int smi_get_pipeline_bytes(size_t *piece_bytes);
 
 /* The local fold kernel: contribs holds `nranks` rows of `count` elements
  * (row r = rank r's contribution, row pitch `ld` elements); out[i] = fold of

@@ -65,6 +65,8 @@ SIGNATURES = {
     "smi_reduce": (I, [SMI_Comm, P, P, SZ, I, I, I, I, P]),
     "smi_reduce_fold": (I, [P, P, I, SZ, SZ, I, I, P]),
     "smi_bcast": (I, [SMI_Comm, P, SZ, I, I, I, P]),
+    "smi_set_pipeline_bytes": (I, [SZ]),
+    "smi_get_pipeline_bytes": (I, [ctypes.POINTER(SZ)]),
     "smi_type_size": (SZ, [I]),
     "smi_scatter": (I, [SMI_Comm, P, P, SZ, I, I, I, P]),
     "smi_gather": (I, [SMI_Comm, P, P, SZ, I, I, I, P]),

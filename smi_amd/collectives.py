@@ -7,6 +7,8 @@ reduce(comm, send, recv, op, root, port) / bcast(comm, buf, root, port).
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -46,6 +48,18 @@ def bcast(comm: Comm, buf: torch.Tensor, root: int = 0, port: int = 0, stream=No
     """Root's `buf` copied into every rank's `buf` (bcast.cl)."""
     _lib.call("smi_bcast", comm.handle, buf.data_ptr(), buf.numel(), _smi_type(buf), root, port,
               _lib.stream_handle(stream))
+
+
+def set_pipeline_bytes(piece_bytes: int) -> None:
+    """Piece size (bytes per owner chunk) of the pipelined reduce/bcast;
+    0 = one piece.  Process-wide, same value on every rank."""
+    _lib.call("smi_set_pipeline_bytes", piece_bytes)
+
+
+def get_pipeline_bytes() -> int:
+    v = ctypes.c_size_t()
+    _lib.call("smi_get_pipeline_bytes", ctypes.byref(v))
+    return v.value
 
 
 def reduce_fold(contribs: torch.Tensor, op="add", out: torch.Tensor | None = None,

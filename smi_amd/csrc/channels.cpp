@@ -535,14 +535,15 @@ int smi_scatter(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count,
                                      hipMemcpyDeviceToDevice, s));
     if (c->size == 1) return SMI_SUCCESS;
     Transport *tp = c->transport.get();
-    SMI_TRY(tp->begin(s));
+    Group grp(tp);
+    SMI_TRY(grp.begin(s));
     if (c->rank == root) {
         for (int k = 0; k < c->size; ++k)
             if (k != root) SMI_TRY(tp->send((const char *)sendbuf + (size_t)k * bytes, bytes, k));
     } else {
         SMI_TRY(tp->recv(recvbuf, bytes, root));
     }
-    return tp->end();
+    return grp.end();
 }
 
 // Bulk point-to-point on device buffers, stream-ordered: the GPU-native form
@@ -586,14 +587,15 @@ int smi_gather(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count, 
                                      hipMemcpyDeviceToDevice, s));
     if (c->size == 1) return SMI_SUCCESS;
     Transport *tp = c->transport.get();
-    SMI_TRY(tp->begin(s));
+    Group grp(tp);
+    SMI_TRY(grp.begin(s));
     if (c->rank == root) {
         for (int k = 0; k < c->size; ++k)
             if (k != root) SMI_TRY(tp->recv((char *)recvbuf + (size_t)k * bytes, bytes, k));
     } else {
         SMI_TRY(tp->send(sendbuf, bytes, root));
     }
-    return tp->end();
+    return grp.end();
 }
 
 
@@ -610,9 +612,10 @@ int smi_send(SMI_Comm comm, const void *buf, size_t count, SMI_Datatype type, in
     if (count == 0) return SMI_SUCCESS;
     SMI_ARG_CHECK(buf, "NULL buffer");
     Transport *tp = c->transport.get();
-    SMI_TRY(tp->begin((hipStream_t)stream));
+    Group grp(tp);
+    SMI_TRY(grp.begin((hipStream_t)stream));
     SMI_TRY(tp->send(buf, count * esz, destination));
-    return tp->end();
+    return grp.end();
 }
 
 int smi_recv(SMI_Comm comm, void *buf, size_t count, SMI_Datatype type, int source, int port, SMI_Stream stream) {
@@ -627,9 +630,10 @@ int smi_recv(SMI_Comm comm, void *buf, size_t count, SMI_Datatype type, int sour
     if (count == 0) return SMI_SUCCESS;
     SMI_ARG_CHECK(buf, "NULL buffer");
     Transport *tp = c->transport.get();
-    SMI_TRY(tp->begin((hipStream_t)stream));
+    Group grp(tp);
+    SMI_TRY(grp.begin((hipStream_t)stream));
     SMI_TRY(tp->recv(buf, count * esz, source));
-    return tp->end();
+    return grp.end();
 }
 
 }  // extern "C"

@@ -228,6 +228,28 @@ static size_t chunk_len(size_t count, size_t cs, int c) {
     return b >= count ? 0 : std::min(cs, count - b);
 }
 
+// Pipelining of smi_reduce / smi_bcast: every owner chunk is cut into n
+// pieces of ps elements (a multiple of 16 bytes, so pieces of an aligned
+// buffer stay aligned).  g_piece_bytes = 0: one piece (no pipelining).
+size_t g_piece_bytes = (size_t)4 << 20;
+struct Pieces {
+    size_t ps;  // elements per piece
+    int n;      // pieces per chunk
+};
+static Pieces pieces_of(size_t cs, size_t esz) {
+    const size_t per16 = 16 / std::min<size_t>(16, esz);
+    size_t want = g_piece_bytes ? std::max<size_t>(g_piece_bytes / esz, 1) : cs;
+    want = (want + per16 - 1) / per16 * per16;
+    const size_t n = (cs + want - 1) / want;
+    size_t ps = (cs + n - 1) / n;  // balanced pieces
+    ps = (ps + per16 - 1) / per16 * per16;
+    return {ps, (int)((cs + ps - 1) / ps)};
+}
+static size_t sub_len(size_t len, size_t ps, int i) {
+    const size_t b = (size_t)i * ps;
+    return b >= len ? 0 : std::min(ps, len - b);
+}
+
 }  // namespace smi
 
 using namespace smi;
@@ -278,41 +300,80 @@ int smi_reduce(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count, 
     }
     const size_t cs = chunk_elems(count, n, esz);
     const size_t my_len = chunk_len(count, cs, me);
-    // workspace: n staging rows of cs elements (+ one result chunk off-root)
+    const Pieces pc = pieces_of(cs, esz);
+    // workspace: two exchange slots of n x ps staging elements, plus the
+    // reduced chunk of a non-root owner (cs elements)
     void *ws = nullptr;
-    SMI_TRY(comm_workspace(c, (size_t)(n + 1) * cs * esz, &ws));
+    SMI_TRY(comm_workspace(c, (2 * (size_t)n * pc.ps + cs) * esz, &ws));
     char *stage = (char *)ws;
-    char *mine = stage + (size_t)n * cs * esz;
+    char *mine = stage + 2 * (size_t)n * pc.ps * esz;
     const char *sb = (const char *)sendbuf;
-    Transport *tp = c->transport.get();
-
-    // 1. owner-chunk exchange: chunk k of my buffer -> owner k
-    SMI_TRY(tp->begin(s));
-    for (int k = 0; k < n; ++k) {
-        if (k == me) continue;
-        SMI_TRY(tp->send(sb + (size_t)k * cs * esz, chunk_len(count, cs, k) * esz, k));
-        SMI_TRY(tp->recv(stage + (size_t)k * cs * esz, my_len * esz, k));
-    }
-    SMI_TRY(tp->end());
-    // 2. canonical rank-order fold of my chunk
     char *dst = (me == root) ? (char *)recvbuf + (size_t)me * cs * esz : mine;
-    if (my_len) {
-        FoldRows rows{};
-        for (int k = 0; k < n; ++k)
-            rows.row[k] = (k == me) ? (const void *)(sb + (size_t)me * cs * esz)
-                                    : (const void *)(stage + (size_t)k * cs * esz);
-        SMI_TRY(launch_fold(rows, dst, n, my_len, type, op, s));
+    Transport *tp = c->transport.get();
+    hipStream_t cs_ = c->comm_stream;
+    auto slot = [&](int i, int k) { return stage + ((size_t)(i & 1) * n + k) * pc.ps * esz; };
+    auto sub = [&](int owner, int i) { return sub_len(chunk_len(count, cs, owner), pc.ps, i); };
+
+    // Pipelined over P pieces (every owner chunk split into P sub-chunks of
+    // ps elements), three stages on two streams:
+    //   comm stream: X(0), X(1), [wait F(0)] {G(0) + X(2)}, [wait F(1)] {G(1) + X(3)} ...
+    //   main stream: [wait X(i)] F(i)
+    // X(i) = owner-chunk exchange of piece i (my sub-chunk i of chunk k ->
+    // owner k) into staging slot i mod 2; F(i) = canonical rank-order fold of
+    // my sub-chunk i (reduce.cl:65-125 with arrival = rank order); G(i) =
+    // the folded piece to the root.  The fold of piece i overlaps the
+    // exchange of piece i+1 (the reference streams its reduce element by
+    // element under a credit window, reduce.cl:13-24,130-179); slot i mod 2
+    // is rewritten by X(i+2) only after F(i), which that group waits for.
+    hipEvent_t ev_s, ev_f, ev_x[3];
+    SMI_TRY(comm_event(c, 2, &ev_s));
+    SMI_TRY(comm_event(c, 3, &ev_f));
+    for (int k = 0; k < 3; ++k) SMI_TRY(comm_event(c, 4 + k, &ev_x[k]));
+    SMI_HIP_CHECK(hipEventRecord(ev_s, s));  // sendbuf is ready on the caller's stream
+    SMI_HIP_CHECK(hipStreamWaitEvent(cs_, ev_s, 0));
+    auto group = [&](int xi, int gi) -> int {  // {X(xi)} + {G(gi)}, either may be -1
+        Group grp(tp);
+        SMI_TRY(grp.begin(cs_));
+        if (xi >= 0)
+            for (int k = 0; k < n; ++k) {
+                if (k == me) continue;
+                SMI_TRY(tp->send(sb + ((size_t)k * cs + (size_t)xi * pc.ps) * esz, sub(k, xi) * esz, k));
+                SMI_TRY(tp->recv(slot(xi, k), sub(me, xi) * esz, k));
+            }
+        if (gi >= 0) {
+            const size_t off = (size_t)gi * pc.ps;
+            if (me == root) {
+                for (int k = 0; k < n; ++k)
+                    if (k != root)
+                        SMI_TRY(tp->recv((char *)recvbuf + ((size_t)k * cs + off) * esz, sub(k, gi) * esz, k));
+            } else {
+                SMI_TRY(tp->send(mine + off * esz, sub(me, gi) * esz, root));
+            }
+        }
+        SMI_TRY(grp.end());
+        if (xi >= 0) SMI_HIP_CHECK(hipEventRecord(ev_x[xi % 3], cs_));
+        return SMI_SUCCESS;
+    };
+    SMI_TRY(group(0, -1));
+    if (pc.n > 1) SMI_TRY(group(1, -1));
+    for (int i = 0; i < pc.n; ++i) {
+        SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_x[i % 3], 0));
+        const size_t len = sub(me, i);
+        if (len) {
+            FoldRows rows{};
+            for (int k = 0; k < n; ++k)
+                rows.row[k] = (k == me) ? (const void *)(sb + ((size_t)me * cs + (size_t)i * pc.ps) * esz)
+                                        : (const void *)slot(i, k);
+            SMI_TRY(launch_fold(rows, dst + (size_t)i * pc.ps * esz, n, len, type, op, s));
+        }
+        SMI_HIP_CHECK(hipEventRecord(ev_f, s));
+        SMI_HIP_CHECK(hipStreamWaitEvent(cs_, ev_f, 0));
+        SMI_TRY(group(i + 2 < pc.n ? i + 2 : -1, i));
     }
-    // 3. gather the reduced chunks on the root
-    SMI_TRY(tp->begin(s));
-    if (me == root) {
-        for (int k = 0; k < n; ++k)
-            if (k != root)
-                SMI_TRY(tp->recv((char *)recvbuf + (size_t)k * cs * esz, chunk_len(count, cs, k) * esz, k));
-    } else {
-        SMI_TRY(tp->send(mine, my_len * esz, root));
-    }
-    return tp->end();
+    // the caller's stream owns the result
+    SMI_HIP_CHECK(hipEventRecord(ev_s, cs_));
+    SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_s, 0));
+    return SMI_SUCCESS;
 }
 
 int smi_bcast(SMI_Comm comm, void *buf, size_t count, SMI_Datatype type, int root, int port,
@@ -338,33 +399,60 @@ int smi_bcast(SMI_Comm comm, void *buf, size_t count, SMI_Datatype type, int roo
     const size_t bytes = count * esz;
 
     if (bytes <= (size_t)256 * 1024 || n == 2) {  // latency-bound: direct fan-out
-        SMI_TRY(tp->begin(s));
+        Group grp(tp);
+        SMI_TRY(grp.begin(s));
         if (me == root) {
             for (int k = 0; k < n; ++k)
                 if (k != root) SMI_TRY(tp->send(b, bytes, k));
         } else {
             SMI_TRY(tp->recv(b, bytes, root));
         }
-        return tp->end();
+        return grp.end();
     }
-    // scatter: the root's chunk k -> rank k (into its own position)
+    // Scatter + all-gather, pipelined over P pieces: group i carries the
+    // scatter of piece i (the root's sub-chunk i of chunk k -> rank k, into
+    // its own position) and the all-gather of piece i-1 (every rank's
+    // sub-chunk to every other rank; the root only sends), so the root's
+    // links scatter while the others exchange -- the reference streams its
+    // broadcast packet by packet (bcast.cl:3-48).
     const size_t cs = chunk_elems(count, n, esz);
-    SMI_TRY(tp->begin(s));
-    if (me == root) {
-        for (int k = 0; k < n; ++k)
-            if (k != root) SMI_TRY(tp->send(b + (size_t)k * cs * esz, chunk_len(count, cs, k) * esz, k));
-    } else {
-        SMI_TRY(tp->recv(b + (size_t)me * cs * esz, chunk_len(count, cs, me) * esz, root));
+    const Pieces pc = pieces_of(cs, esz);
+    auto sub = [&](int owner, int i) { return sub_len(chunk_len(count, cs, owner), pc.ps, i); };
+    auto at = [&](int owner, int i) { return b + ((size_t)owner * cs + (size_t)i * pc.ps) * esz; };
+    for (int i = 0; i <= pc.n; ++i) {
+        Group grp(tp);
+        SMI_TRY(grp.begin(s));
+        if (i < pc.n) {  // scatter of piece i
+            if (me == root) {
+                for (int k = 0; k < n; ++k)
+                    if (k != root) SMI_TRY(tp->send(at(k, i), sub(k, i) * esz, k));
+            } else {
+                SMI_TRY(tp->recv(at(me, i), sub(me, i) * esz, root));
+            }
+        }
+        if (i > 0) {  // all-gather of piece i-1
+            const int g = i - 1;
+            for (int k = 0; k < n; ++k) {
+                if (k == me) continue;
+                if (k != root) SMI_TRY(tp->send(at(me, g), sub(me, g) * esz, k));
+                if (me != root) SMI_TRY(tp->recv(at(k, g), sub(k, g) * esz, k));
+            }
+        }
+        SMI_TRY(grp.end());
     }
-    SMI_TRY(tp->end());
-    // all-gather among the ranks; the root only sends its own chunk
-    SMI_TRY(tp->begin(s));
-    for (int k = 0; k < n; ++k) {
-        if (k == me) continue;
-        if (k != root) SMI_TRY(tp->send(b + (size_t)me * cs * esz, chunk_len(count, cs, me) * esz, k));
-        if (me != root) SMI_TRY(tp->recv(b + (size_t)k * cs * esz, chunk_len(count, cs, k) * esz, k));
-    }
-    return tp->end();
+    return SMI_SUCCESS;
+}
+
+int smi_set_pipeline_bytes(size_t piece_bytes) {
+    SMI_ARG_CHECK(piece_bytes == 0 || piece_bytes >= 16, "piece_bytes must be 0 (no pipelining) or >= 16");
+    g_piece_bytes = piece_bytes;
+    return SMI_SUCCESS;
+}
+
+int smi_get_pipeline_bytes(size_t *piece_bytes) {
+    SMI_ARG_CHECK(piece_bytes, "NULL output");
+    *piece_bytes = g_piece_bytes;
+    return SMI_SUCCESS;
 }
 
 }  // extern "C"

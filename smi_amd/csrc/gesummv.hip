@@ -180,14 +180,15 @@ int smi_gesummv(SMI_Comm comm, const float *A_rows, const float *B_rows, const f
     // stream the partial y chunks to the root (the rank-1 SMI_Push of
     // beta*B*x and rank-0 SMI_Pop in the reference)
     Transport *tp = c->transport.get();
-    SMI_TRY(tp->begin(s));
+    Group grp(tp);
+    SMI_TRY(grp.begin(s));
     if (me == root) {
         for (int k = 0; k < n; ++k)
             if (k != root) SMI_TRY(tp->recv(y + row0(k), (size_t)(row0(k + 1) - row0(k)) * sizeof(float), k));
     } else {
         SMI_TRY(tp->send(ychunk, (size_t)my_n * sizeof(float), root));
     }
-    return tp->end();
+    return grp.end();
 }
 
 }  // extern "C"

@@ -71,6 +71,32 @@ class Transport {
     virtual int recv_now(void *buf, size_t bytes, int peer, hipStream_t stream) = 0;
 };
 
+// One transport group, closed on every path: begin() takes the transport's
+// bulk lock (two host threads never interleave groups on one communicator)
+// and end() -- or the destructor, on an early error return -- releases it.
+class Group {
+  public:
+    explicit Group(Transport *t) : t_(t) {}
+    Group(const Group &) = delete;
+    Group &operator=(const Group &) = delete;
+    int begin(hipStream_t s) {
+        const int rc = t_->begin(s);
+        open_ = rc == SMI_SUCCESS;
+        return rc;
+    }
+    int end() {
+        open_ = false;
+        return t_->end();
+    }
+    ~Group() {
+        if (open_) t_->end();
+    }
+
+  private:
+    Transport *t_;
+    bool open_ = false;
+};
+
 std::unique_ptr<Transport> make_rccl_transport(int rank, int size,
                                                const void *unique_id,
                                                int id_bytes, int *rc);

@@ -23,7 +23,8 @@ static int exchange1(Comm *c, const Neighbours &nb, const float *tile, int rows,
                      hipStream_t s) {
     Transport *tp = c->transport.get();
     const size_t rb = (size_t)cols * sizeof(float), cb = (size_t)rows * sizeof(float);
-    SMI_TRY(tp->begin(s));
+    Group grp(tp);
+    SMI_TRY(grp.begin(s));
     if (nb.top >= 0) {
         SMI_TRY(tp->send(tile, rb, nb.top));
         SMI_TRY(tp->recv(h_top, rb, nb.top));
@@ -40,7 +41,7 @@ static int exchange1(Comm *c, const Neighbours &nb, const float *tile, int rows,
         SMI_TRY(tp->send(s_right, cb, nb.right));
         SMI_TRY(tp->recv(h_right, cb, nb.right));
     }
-    return tp->end();
+    return grp.end();
 }
 
 // Depth-2 exchange (once per pair of steps): two rows / two columns per
@@ -67,7 +68,8 @@ static int exchange2(Comm *c, const Neighbours &nb, const float *tile, int rows,
                      hipStream_t s) {
     Transport *tp = c->transport.get();
     const size_t rb = 2 * (size_t)cols * sizeof(float), cb = 2 * (size_t)rows * sizeof(float);
-    SMI_TRY(tp->begin(s));
+    Group grp(tp);
+    SMI_TRY(grp.begin(s));
     if (nb.top >= 0) {
         SMI_TRY(tp->send(tile, rb, nb.top));
         SMI_TRY(tp->recv(h.top2, rb, nb.top));
@@ -90,7 +92,7 @@ static int exchange2(Comm *c, const Neighbours &nb, const float *tile, int rows,
         SMI_TRY(tp->send(h.send_corner + k, sizeof(float), diag[k]));
         SMI_TRY(tp->recv(h.corner + k, sizeof(float), diag[k]));
     }
-    return tp->end();
+    return grp.end();
 }
 
 // Depth-K exchange (once per K steps): K rows / K columns per side
@@ -132,7 +134,8 @@ static int exchangek(Comm *c, const Neighbours &nb, const float *tile, int rows,
         return launch_multicopy(src, dst, by, 8, s);
     }
 #endif
-    SMI_TRY(tp->begin(s));
+    Group grp(tp);
+    SMI_TRY(grp.begin(s));
     if (nb.top >= 0) {
         SMI_TRY(tp->send(tile, rb, nb.top));
         SMI_TRY(tp->recv(h.top, rb, nb.top));
@@ -155,7 +158,7 @@ static int exchangek(Comm *c, const Neighbours &nb, const float *tile, int rows,
         SMI_TRY(tp->send(h.send_corner[k], kb, diag[k]));
         SMI_TRY(tp->recv(h.corner[k], kb, diag[k]));
     }
-    return tp->end();
+    return grp.end();
 }
 
 static int ensure_halo(Comm *c, size_t elems) {

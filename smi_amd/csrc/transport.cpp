@@ -17,6 +17,7 @@
 #include <deque>
 #include <map>
 #include <mutex>
+#include <tuple>
 
 #include "smi_internal.h"
 
@@ -25,13 +26,27 @@ namespace smi {
 // ================================================================= RCCL ==
 class RcclTransport final : public Transport {
   public:
-    explicit RcclTransport(ncclComm_t c) : comm_(c) {}
+    // `chan`: a second communicator over the same ranks (ncclCommSplit) that
+    // carries only the element-granular channel packets, so they never
+    // match a bulk receive of a collective or a stencil exchange -- the
+    // reference's ports keep those streams apart the same way (one FIFO
+    // per port).
+    RcclTransport(ncclComm_t c, ncclComm_t chan) : comm_(c), chan_(chan) {}
     ~RcclTransport() override {
+        if (chan_) ncclCommDestroy(chan_);
         if (comm_) ncclCommDestroy(comm_);
     }
+    // begin() holds the bulk mutex until end(): two host threads can never
+    // interleave their groups on the one RCCL communicator (RCCL
+    // communicators are not thread-safe).  Matching stays in issue order per
+    // rank pair, so every rank must issue its bulk operations in the same
+    // order (include/smi/communicator.h).
     int begin(hipStream_t stream) override {
+        bulk_mu_.lock();
         stream_ = stream;
-        return check(ncclGroupStart(), "ncclGroupStart");
+        const int rc = check(ncclGroupStart(), "ncclGroupStart");
+        if (rc != SMI_SUCCESS) bulk_mu_.unlock();
+        return rc;
     }
     int send(const void *buf, size_t bytes, int peer) override {
         if (bytes == 0) return SMI_SUCCESS;
@@ -41,15 +56,24 @@ class RcclTransport final : public Transport {
         if (bytes == 0) return SMI_SUCCESS;
         return check(ncclRecv(buf, bytes, ncclUint8, peer, comm_, stream_), "ncclRecv");
     }
-    int end() override { return check(ncclGroupEnd(), "ncclGroupEnd"); }
+    int end() override {
+        const int rc = check(ncclGroupEnd(), "ncclGroupEnd");
+        bulk_mu_.unlock();
+        return rc;
+    }
 
-    // Small sends complete into the peer's connection FIFO without a posted
-    // receive, so a detached send only needs an event to tell when the
-    // staging buffer may be reused.
+    // Channel packets travel on `chan_`, whose connections to every peer
+    // were set up at init (connect_all), so a send never waits for a
+    // connection handshake with a peer that is busy elsewhere.  A packet
+    // (2 KiB) fits one slot of the connection's FIFO, so the send completes
+    // without a posted receive while the peer has fewer than NCCL_STEPS (8)
+    // unpopped packets from this rank; past that the send stream stalls
+    // until the peer pops -- the credit window of push.cl:21-31.  The
+    // ticket's event tells when the staging slot may be reused.
     int send_detached(const void *buf, size_t bytes, int peer, hipStream_t stream, SendTicket *t) override {
-        std::lock_guard<std::mutex> lk(mu_);  // RCCL communicators are not thread-safe
+        std::lock_guard<std::mutex> lk(chan_mu_);
         SMI_TRY(check(ncclGroupStart(), "ncclGroupStart"));
-        SMI_TRY(check(ncclSend(buf, bytes, ncclUint8, peer, comm_, stream), "ncclSend"));
+        SMI_TRY(check(ncclSend(buf, bytes, ncclUint8, peer, chan_, stream), "ncclSend"));
         SMI_TRY(check(ncclGroupEnd(), "ncclGroupEnd"));
         if (!t->ev) SMI_HIP_CHECK(hipEventCreateWithFlags(&t->ev, hipEventDisableTiming));
         SMI_HIP_CHECK(hipEventRecord(t->ev, stream));
@@ -63,10 +87,36 @@ class RcclTransport final : public Transport {
         return SMI_SUCCESS;
     }
     int recv_now(void *buf, size_t bytes, int peer, hipStream_t stream) override {
-        std::lock_guard<std::mutex> lk(mu_);
+        std::lock_guard<std::mutex> lk(chan_mu_);
         SMI_TRY(check(ncclGroupStart(), "ncclGroupStart"));
-        SMI_TRY(check(ncclRecv(buf, bytes, ncclUint8, peer, comm_, stream), "ncclRecv"));
+        SMI_TRY(check(ncclRecv(buf, bytes, ncclUint8, peer, chan_, stream), "ncclRecv"));
         return check(ncclGroupEnd(), "ncclGroupEnd");
+    }
+
+    // One byte to and from every peer on the channel communicator: RCCL
+    // connects point-to-point peers lazily inside ncclGroupEnd, with a
+    // handshake both sides must join; doing it here, collectively, means no
+    // later detached send depends on what its peer is doing.
+    int connect_all(int rank, int size) {
+        if (size == 1) return SMI_SUCCESS;
+        char *d = nullptr;
+        hipStream_t st = nullptr;
+        SMI_HIP_CHECK(hipMalloc(&d, 2 * (size_t)size));
+        int rc = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess ? SMI_SUCCESS : SMI_ERR_HIP;
+        if (rc == SMI_SUCCESS) rc = check(ncclGroupStart(), "ncclGroupStart");
+        for (int p = 0; p < size && rc == SMI_SUCCESS; ++p) {
+            if (p == rank) continue;
+            rc = check(ncclSend(d + p, 1, ncclUint8, p, chan_, st), "ncclSend");
+            if (rc == SMI_SUCCESS) rc = check(ncclRecv(d + size + p, 1, ncclUint8, p, chan_, st), "ncclRecv");
+        }
+        if (rc == SMI_SUCCESS) rc = check(ncclGroupEnd(), "ncclGroupEnd");
+        if (rc == SMI_SUCCESS && hipStreamSynchronize(st) != hipSuccess) {
+            set_error("channel connect: stream synchronize failed");
+            rc = SMI_ERR_HIP;
+        }
+        if (st) hipStreamDestroy(st);
+        hipFree(d);
+        return rc;
     }
 
     static int check(ncclResult_t r, const char *what) {
@@ -76,9 +126,9 @@ class RcclTransport final : public Transport {
     }
 
   private:
-    ncclComm_t comm_ = nullptr;
+    ncclComm_t comm_ = nullptr, chan_ = nullptr;
     hipStream_t stream_ = nullptr;
-    std::mutex mu_;
+    std::mutex bulk_mu_, chan_mu_;
 };
 
 std::unique_ptr<Transport> make_rccl_transport(int rank, int size,
@@ -91,10 +141,18 @@ std::unique_ptr<Transport> make_rccl_transport(int rank, int size,
     }
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof(id));
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr, chan = nullptr;
     *rc = RcclTransport::check(ncclCommInitRank(&comm, size, id, rank), "ncclCommInitRank");
     if (*rc != SMI_SUCCESS) return nullptr;
-    return std::make_unique<RcclTransport>(comm);
+    *rc = RcclTransport::check(ncclCommSplit(comm, 0, rank, &chan, nullptr), "ncclCommSplit");
+    if (*rc != SMI_SUCCESS) {
+        ncclCommDestroy(comm);
+        return nullptr;
+    }
+    auto t = std::make_unique<RcclTransport>(comm, chan);
+    *rc = t->connect_all(rank, size);
+    if (*rc != SMI_SUCCESS) return nullptr;
+    return t;
 }
 
 // ================================================================ local ==
@@ -113,7 +171,9 @@ struct LocalGroup {
     int size = 0;
     std::mutex mu;
     std::condition_variable cv;
-    std::map<std::pair<int, int>, std::deque<std::shared_ptr<Post>>> mailbox;
+    // (src, dst, space): space 0 = bulk groups, 1 = element-channel packets
+    // (send_detached / recv_now), matched FIFO within each space only
+    std::map<std::tuple<int, int, int>, std::deque<std::shared_ptr<Post>>> mailbox;
     int joined = 0;
 };
 
@@ -138,7 +198,9 @@ class LocalTransport final : public Transport {
   public:
     LocalTransport(std::shared_ptr<LocalGroup> g, int rank) : g_(std::move(g)), rank_(rank) {}
 
+    // begin() .. end() hold the bulk mutex (see RcclTransport::begin)
     int begin(hipStream_t stream) override {
+        bulk_mu_.lock();
         stream_ = stream;
         sends_.clear();
         recvs_.clear();
@@ -168,6 +230,11 @@ class LocalTransport final : public Transport {
     // wait for the `done` of each of our sends, so later work may reuse the
     // send buffers.
     int end() override {
+        const int rc = end_group();
+        bulk_mu_.unlock();
+        return rc;
+    }
+    int end_group() {
         std::vector<std::shared_ptr<Post>> mine;
         for (auto &s : sends_) {
             auto p = std::make_shared<Post>();
@@ -181,13 +248,13 @@ class LocalTransport final : public Transport {
         {
             std::lock_guard<std::mutex> lk(g_->mu);
             for (size_t i = 0; i < sends_.size(); ++i)
-                g_->mailbox[{rank_, sends_[i].peer}].push_back(mine[i]);
+                g_->mailbox[{rank_, sends_[i].peer, 0}].push_back(mine[i]);
         }
         g_->cv.notify_all();
 
         int rc = SMI_SUCCESS;
         for (auto &r : recvs_) {
-            const int st = take(r.buf, r.bytes, r.peer, stream_);
+            const int st = take(r.buf, r.bytes, r.peer, 0, stream_);
             if (st != SMI_SUCCESS && rc == SMI_SUCCESS) rc = st;
         }
         for (auto &p : mine) {
@@ -221,7 +288,7 @@ class LocalTransport final : public Transport {
         SMI_HIP_CHECK(hipEventRecord(p->ready, stream));
         {
             std::lock_guard<std::mutex> lk(g_->mu);
-            g_->mailbox[{rank_, peer}].push_back(p);
+            g_->mailbox[{rank_, peer, 1}].push_back(p);
         }
         g_->cv.notify_all();
         t->impl = p;
@@ -233,7 +300,7 @@ class LocalTransport final : public Transport {
             set_error("recv: peer out of range");
             return SMI_ERR_INVALID_ARG;
         }
-        return take(buf, bytes, peer, stream);
+        return take(buf, bytes, peer, 1, stream);
     }
     int ticket_wait(SendTicket *t) override {
         if (!t->live) return SMI_SUCCESS;
@@ -277,11 +344,11 @@ class LocalTransport final : public Transport {
     // Wait for the next post from `peer` (FIFO per (src, dst), like the
     // reference's per-port FIFO order), order `stream` after the sender's
     // `ready` event, copy, and mark the post consumed.
-    int take(void *buf, size_t bytes, int peer, hipStream_t stream) {
+    int take(void *buf, size_t bytes, int peer, int space, hipStream_t stream) {
         std::shared_ptr<Post> p;
         {
             std::unique_lock<std::mutex> lk(g_->mu);
-            auto &q = g_->mailbox[{peer, rank_}];
+            auto &q = g_->mailbox[{peer, rank_, space}];
             g_->cv.wait(lk, [&] { return !q.empty(); });
             p = q.front();
             q.pop_front();
@@ -312,6 +379,7 @@ class LocalTransport final : public Transport {
     };
     std::shared_ptr<LocalGroup> g_;
     int rank_;
+    std::mutex bulk_mu_;
     hipStream_t stream_ = nullptr;
     std::vector<Op> sends_, recvs_;
 };

@@ -129,3 +129,38 @@ def test_bcast_large_scatter_allgather(gpu, n):
     for root in (0, n - 1):
         for got in _group_bcast(n, data, root):
             assert np.array_equal(got, data)
+
+
+@pytest.fixture
+def piece_bytes():
+    """Set the reduce/bcast pipeline piece size for one test, restore after."""
+    from smi_amd import collectives
+    old = collectives.get_pipeline_bytes()
+    yield collectives.set_pipeline_bytes
+    collectives.set_pipeline_bytes(old)
+
+
+@pytest.mark.parametrize("pb", [0, 16, 1024, 4 << 20])
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_reduce_pipelined_pieces_bit_identical(gpu, oracle_mod, piece_bytes, pb, n):
+    """The piece size changes the schedule only: every setting (one piece,
+    16-byte pieces, many 1 KiB pieces, the 4 MiB default) gives the oracle's
+    canonical fold bit for bit, ragged counts included."""
+    piece_bytes(pb)
+    for t in (1, 2, 3):
+        for count in (5, 100003):
+            c = _contribs(oracle_mod, n, count, t, seed=count + n + t)
+            root = (count + t) % n
+            got = _group_reduce(n, list(c), t, 0, root)
+            assert np.array_equal(got.view(np.uint8), oracle_mod.reduce(c, t, 0).view(np.uint8)), (pb, t, count)
+
+
+@pytest.mark.parametrize("pb", [0, 16, 4096])
+@pytest.mark.parametrize("n", [3, 8])
+def test_bcast_pipelined_pieces(gpu, piece_bytes, pb, n):
+    piece_bytes(pb)
+    rng = np.random.default_rng(pb + n)
+    data = rng.integers(0, 1 << 30, size=(1 << 18) + 7, dtype=np.int32)  # 1 MiB: scatter + all-gather
+    for root in (0, n - 1):
+        for got in _group_bcast(n, data, root):
+            assert np.array_equal(got, data)
