@@ -27,15 +27,20 @@ The JSON line also carries:
                    from the rocprofv3 PMC passes committed under profiles/ and
                    `hbm_frac` = traffic / launch time / peak
   cpu_baseline  -- the oracle's C restatement of the reference stencil
-                   (OpenMP) timed on this host on a bounded sample (rank 0,
-                   N=1 only)
+                   (OpenMP, every thread of this job's CPU share) timed on
+                   this host on a bounded sample (rank 0, N=1 only), with the
+                   CPU model / nproc and the serial Reference()-order and
+                   rank-decomposed (emulator) legs; aux.cpu: reduce and
+                   gesummv CPU legs
   halo          -- (N>1) xGMI bytes per step of the halo exchange and the
                    per-link rate the measured step time demands
   aux           -- measured after the timed stencil region (skip: --no-aux):
                    gesummv 32768^2 row-sharded over the N GPUs (BASELINE
                    config 5) and, for N>1, SMI_Reduce int32/fp32 and SMI_Bcast
                    at 4 KiB-256 MiB (config 4) with algbw vs the xGMI bound,
-                   and the p2p bandwidth/latency microbenchmarks on one link;
+                   and the p2p bandwidth/latency microbenchmarks on one link,
+                   each with mean / stddev / 99 % CI over its runs (the
+                   reference harness's statistics);
                    bounded by a watchdog so the stencil line always prints
 """
 from __future__ import annotations
@@ -84,29 +89,110 @@ def decomposition(n: int) -> tuple[int, int]:
     return px, n // px
 
 
-def cpu_baseline(budget_s: float = 2.0) -> dict:
-    """Oracle (C restatement of the reference stencil, all host threads):
-    chunks of steps until about budget_s of wall time has passed (x threads
-    = ~20-30 core-seconds)."""
-    import oracle
-    threads = min(16, os.cpu_count() or 1)
-    g = oracle.init_uniform(TILE, TILE, seed=42)
-    oracle.stencil(g, 2, threads=threads)  # warm: page faults, thread pool
-    steps, dt = 0, 0.0
-    chunk = 4
-    while dt < budget_s:
+def host_cpu() -> dict:
+    """The host's processor: model (/proc/cpuinfo), nproc, the CPUs this
+    process may run on, and the thread count the CPU legs use (the box's
+    OMP_NUM_THREADS share when set, else every CPU of the affinity mask)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = int(omp) if omp.isdigit() and int(omp) > 0 else affinity
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity, "threads": threads}
+
+
+def _time_loop(fn, budget_s: float, min_reps: int = 1):
+    """Repeat fn until budget_s of wall time (at least min_reps); returns
+    (reps, seconds)."""
+    fn()  # warm: page faults, thread pool
+    reps, dt = 0, 0.0
+    while dt < budget_s or reps < min_reps:
         t0 = time.perf_counter()
-        g = oracle.stencil(g, chunk, threads=threads)
+        fn()
         dt += time.perf_counter() - t0
-        steps += chunk
-    return {
+        reps += 1
+    return reps, dt
+
+
+def cpu_baseline(budget_s: float = 2.0) -> dict:
+    """CPU baselines of SURVEY §8(d) / BASELINE.md §3, all on the oracle's C
+    restatement (the reference's own CPU path -- Intel FPGA emulator + MPI --
+    cannot be built here or on the box):
+      value       -- the stencil on every host thread this job may use
+                     (OpenMP), 8192^2 tile, chunks of 4 steps for ~budget_s;
+      legs.serial_reference_order -- the host Reference() loop order
+                     (examples/host/stencil_smi.cpp:33-46) on 1 core;
+      legs.emulator_config1 / emulator_2x4 -- the rank-decomposed program
+                     (Read/Stencil/Write per rank, halo queues: the threads-
+                     as-ranks emulator semantics) for config 1 (256^2, 2x2,
+                     T=32) and a 2x4 grid of 256^2 tiles, 1 core."""
+    import oracle
+    cpu = host_cpu()
+    threads = cpu["threads"]
+    g = oracle.init_uniform(TILE, TILE, seed=42)
+    state = {"g": g}
+
+    def omp_chunk():
+        state["g"] = oracle.stencil(state["g"], 4, threads=threads)
+
+    reps, dt = _time_loop(omp_chunk, budget_s)
+    steps = 4 * reps
+    out = {
         "value": round(TILE * TILE * steps / dt / 1e9, 3),
         "unit": "GCell/s",
         "cores": threads,
         "kind": "port",
         "sample": f"{TILE}x{TILE} fp32 Jacobi, {steps} steps, OpenMP C restatement "
                   f"(oracle/smi_oracle.c) of stencil_smi.cl:117-165, {dt:.1f} s wall on {threads} threads",
+        **cpu,
     }
+    legs = {}
+    gs = g[:2048, :2048].copy()
+    reps, dt = _time_loop(lambda: oracle.stencil(gs, 2, order="host", threads=1), 1.5)
+    legs["serial_reference_order"] = {
+        "GCells": round(2048 * 2048 * 2 * reps / dt / 1e9, 4), "cores": 1,
+        "sample": f"2048x2048, {2 * reps} steps in {dt:.2f} s, host Reference() order (stencil_smi.cpp:33-46)"}
+    for name, (X, Y, PX, PY) in (("emulator_config1", (256, 256, 2, 2)), ("emulator_2x4", (512, 1024, 2, 4))):
+        ge = oracle.init_uniform(X, Y, seed=5)
+        reps, dt = _time_loop(lambda: oracle.stencil_decomposed(ge, 32, PX, PY), 0.5, 3)
+        legs[name] = {"GCells": round(X * Y * 32 * reps / dt / 1e9, 4), "ms_per_program": round(dt / reps * 1e3, 3),
+                      "cores": 1, "sample": f"{X}x{Y} as {PX}x{PY} ranks of {X // PX}x{Y // PY}, 32 steps, "
+                                            f"{reps} programs"}
+    out["legs"] = legs
+    return out
+
+
+def cpu_aux_legs(budget_s: float = 1.0) -> dict:
+    """CPU legs of the auxiliary configs on the oracle: the canonical reduce
+    fold (reduce.cl:42-148) of 8 contributions, and one 8-way gesummv row
+    shard (4096 x 32768, gesummv_rank0.cl:53-203) on every host thread."""
+    import oracle
+    cpu = host_cpu()
+    n, count = 8, 16 << 20
+    c = np.random.default_rng(3).random((n, count), dtype=np.float32)
+    reps, dt = _time_loop(lambda: oracle.reduce(c, 2, 0), budget_s)
+    red = {"GBs": round(4 * (n + 1) * count * reps / dt / 1e9, 3), "cores": 1,
+           "sample": f"{n} x {count} fp32 add, {reps} folds in {dt:.2f} s (algorithmic bytes 4(n+1) per element)"}
+    del c
+    rows, m = GESUMMV_N // 8, GESUMMV_N
+    rng = np.random.default_rng(4)
+    A = rng.random((rows, m), dtype=np.float32)
+    B = rng.random((rows, m), dtype=np.float32)
+    x = rng.random(m, dtype=np.float32)
+    reps, dt = _time_loop(lambda: oracle.gesummv(A, B, x, 1.5, 0.5, threads=cpu["threads"]), budget_s)
+    gem = {"GBs": round(4 * (2 * rows * m + m + rows) * reps / dt / 1e9, 3), "cores": cpu["threads"],
+           "ms": round(dt / reps * 1e3, 3), "sample": f"{rows}x{m} row shard (A and B), {reps} runs"}
+    return {"reduce_fold_f32": red, "gesummv_shard": gem, "kind": "port", **cpu}
 
 
 def pmc_traffic(cells: int, steps_per_launch: int) -> float | None:
@@ -174,6 +260,34 @@ def _timed(fn, iters: int, barrier, world: int) -> float:
     return dt
 
 
+def _timed_runs(fn, runs: int, barrier, world: int) -> dict:
+    """The reference harness's statistics (microbenchmarks/host/
+    reduce_benchmark.cpp:120-155): `runs` runs, each bracketed by a barrier +
+    device sync and timed as the max over ranks; mean, population stddev and
+    the 99 % confidence half-width 2.58 * stddev / sqrt(runs), in us."""
+    import torch
+    import torch.distributed as dist
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(runs):
+        barrier()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    if world > 1:
+        t = torch.tensor(ts, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ts = [float(v) for v in t]
+    us = np.array(ts) * 1e6
+    mean = float(us.mean())
+    sd = float(np.sqrt(((us - mean) ** 2).mean()))
+    ci = 2.58 * sd / np.sqrt(len(us))
+    return {"us": round(mean, 2), "stddev_us": round(sd, 2), "ci99_us": round(ci, 2),
+            "ci99_pct_of_mean": round(100 * ci / mean, 2), "runs": len(us), "mean_s": mean * 1e-6}
+
+
 def _all_ok(ok: bool, world: int) -> bool:
     """A check made on one rank, agreed by every rank (rank 0 prints)."""
     if world == 1:
@@ -237,13 +351,12 @@ def aux_p2p(comm, world: int, rank: int, stream, barrier) -> dict:
                 collectives.recv(comm, buf, 0, stream=stream)
 
         with torch.cuda.stream(stream):
-            t = _timed(call, 20 if nbytes <= (1 << 20) else 5, barrier, world)
+            st = _timed_runs(call, 30 if nbytes <= (1 << 20) else 10, barrier, world)
         ok = True
         if rank == 1:
             ok = bool((buf == start + torch.arange(n, dtype=torch.float64, device="cuda")).all().item())
-        gbs = nbytes / t / 1e9
-        row = {"bytes": nbytes, "us": round(t * 1e6, 1), "GBs": round(gbs, 2),
-               "link_frac": round(gbs / XGMI_LINK_GBS, 4)}
+        gbs = nbytes / st.pop("mean_s") / 1e9
+        row = {"bytes": nbytes, **st, "GBs": round(gbs, 2), "link_frac": round(gbs / XGMI_LINK_GBS, 4)}
         if not _all_ok(ok, world):
             row["error"] = "KAT mismatch on rank 1"
         bw.append(row)
@@ -262,9 +375,12 @@ def aux_p2p(comm, world: int, rank: int, stream, barrier) -> dict:
                 collectives.send(comm, v, 0, stream=stream)
 
     with torch.cuda.stream(stream):
-        t = _timed(pingpong, 1, barrier, world)
-    return {"pair": [0, 1], "bandwidth": bw, "latency_us": round(t / (2 * trips) * 1e6, 2),
-            "note": "latency = ping-pong round trip / 2 of one int32, stream-ordered smi_send/smi_recv"}
+        st = _timed_runs(pingpong, 10, barrier, world)
+    st.pop("mean_s")
+    lat = {k: (round(v / (2 * trips), 3) if k.endswith("_us") or k == "us" else v) for k, v in st.items()}
+    return {"pair": [0, 1], "bandwidth": bw, "latency_us": lat["us"], "latency": lat,
+            "note": "latency = ping-pong round trip / 2 of one int32 (runs of 100 round trips), stream-ordered "
+                    "smi_send/smi_recv; stats per the reference harness (mean, population stddev, 99 % CI)"}
 
 
 def aux_collectives(comm, world: int, rank: int, stream, barrier) -> list:
@@ -278,7 +394,7 @@ def aux_collectives(comm, world: int, rank: int, stream, barrier) -> list:
     root = world - 1
     for nbytes in COLL_BYTES:
         count = nbytes // 4
-        iters = 20 if nbytes <= (1 << 20) else 5
+        iters = 30 if nbytes <= (1 << 20) else 10
         snd_i = torch.full((count,), rank + 1, dtype=torch.int32, device="cuda")
         snd_f = torch.rand(count, device="cuda")
         rcv = torch.empty(count, dtype=torch.float32, device="cuda") if rank == root else None
@@ -286,18 +402,18 @@ def aux_collectives(comm, world: int, rank: int, stream, barrier) -> list:
         buf = torch.rand(count, device="cuda")
         torch.cuda.synchronize()
         with torch.cuda.stream(stream):
-            t_ri = _timed(lambda: collectives.reduce(comm, snd_i, rcv_i, "add", root=root, stream=stream),
-                          iters, barrier, world)
-            t_rf = _timed(lambda: collectives.reduce(comm, snd_f, rcv, "add", root=root, stream=stream),
-                          iters, barrier, world)
-            t_b = _timed(lambda: collectives.bcast(comm, buf, root=0, stream=stream), iters, barrier, world)
+            t_ri = _timed_runs(lambda: collectives.reduce(comm, snd_i, rcv_i, "add", root=root, stream=stream),
+                               iters, barrier, world)
+            t_rf = _timed_runs(lambda: collectives.reduce(comm, snd_f, rcv, "add", root=root, stream=stream),
+                               iters, barrier, world)
+            t_b = _timed_runs(lambda: collectives.bcast(comm, buf, root=0, stream=stream), iters, barrier, world)
         ok = True
         if rank == root:  # KAT: sum of (rank + 1) = n(n+1)/2 (microbenchmarks/kernels/reduce.cl:13-24)
             ok = bool((rcv_i == world * (world + 1) // 2).all().item())
         bound = world * XGMI_LINK_GBS / 2
-        for op, t in (("reduce_i32_add", t_ri), ("reduce_f32_add", t_rf), ("bcast_f32", t_b)):
-            gbs = nbytes / t / 1e9
-            out.append({"op": op, "bytes": nbytes, "us": round(t * 1e6, 1), "algbw_GBs": round(gbs, 2),
+        for op, st in (("reduce_i32_add", t_ri), ("reduce_f32_add", t_rf), ("bcast_f32", t_b)):
+            gbs = nbytes / st.pop("mean_s") / 1e9
+            out.append({"op": op, "bytes": nbytes, **st, "algbw_GBs": round(gbs, 2),
                         "xgmi_bound_GBs": bound, "xgmi_frac": round(gbs / bound, 4)})
         if not _all_ok(ok, world):
             out.append({"op": "reduce_i32_add", "bytes": nbytes, "error": "KAT mismatch on the root"})
@@ -423,7 +539,13 @@ def main() -> None:
         kernel_name = dom["kernel"]
     else:
         spl, cells_launch, bytes_launch, sweep_avg_ms, achieved, kernel_name = 0, 0, 0, 0.0, 0.0, None
-    traffic = pmc_traffic(cells_per_gpu, spl) if world == 1 and dom else None
+    traffic = pmc_traffic(cells_per_gpu, spl) if dom else None
+    traffic_basis = "measured (rocprofv3 PMC, this tile and kernel)" if traffic else None
+    if traffic and world > 1 and cells_launch:
+        # the multi-rank interior sweep covers the tile minus K-wide halo
+        # bands: the 1x1 pass's measured bytes scaled by the cells it stores
+        traffic *= cells_launch / cells_per_gpu
+        traffic_basis = "1x1 PMC pass scaled by the interior's cells per launch (estimate)"
     out = {
         "metric": "Jacobi stencil GCell/s (8192^2 fp32 per GPU)",
         "value": round(value, 2),
@@ -458,6 +580,7 @@ def main() -> None:
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_basis": traffic_basis,
             "kernel": kernel_name,
             "kernel_avg_ms": round(sweep_avg_ms, 5),
             "launches": dom["launches"] if dom else 0,
@@ -480,7 +603,7 @@ def main() -> None:
     if traffic and sweep_avg_ms:
         hbm = traffic / (sweep_avg_ms * 1e-3) / 1e9
         out["roofline"]["hbm_achieved"] = round(hbm, 1)
-        out["roofline"]["hbm_frac"] = round(hbm / HBM_PEAK_GBS, 4)
+        out["roofline"]["hbm_frac"] = round(hbm / HBM_PEAK_GBS, 4)  # per GPU
     if world > 1:
         out["halo"] = halo_report(PX, PY, X, Y, max(spl, 1), elapsed / args.steps * 1e3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -511,6 +634,8 @@ def main() -> None:
             if world > 1:
                 aux["collectives"] = aux_collectives(comm, world, rank, stream, barrier)
                 aux["p2p"] = aux_p2p(comm, world, rank, stream, barrier)
+            elif rank == 0 and not args.no_cpu_baseline:
+                aux["cpu"] = cpu_aux_legs()
         except Exception as e:  # report, never lose the stencil line
             aux["error"] = f"{type(e).__name__}: {e}"
         out["aux"] = aux

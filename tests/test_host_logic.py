@@ -199,6 +199,15 @@ def _worker(rank, world, port, PX, PY, T, q):
         uid = exchange_unique_id(rank, world, dist.distributed_c10d._get_default_store(), key="t/uid")
         ids = [None] * world
         dist.all_gather_object(ids, uid)
+        # the production bring-up itself: Comm.from_env exchanges a fresh id
+        # through the same store and calls smi_init, which must fail loudly
+        # here (no GPU: the product path has no CPU fallback)
+        import smi_amd
+        try:
+            smi_amd.Comm.from_env(device=0)
+            no_gpu_fails = False
+        except smi_amd.SMIError:
+            no_gpu_fails = True
         XL, YL = 24, 28
         g = o.init_uniform(XL * PX, YL * PY, seed=9)
         ipx, ipy = rank // PY, rank % PY
@@ -214,7 +223,8 @@ def _worker(rank, world, port, PX, PY, T, q):
         dist.all_gather_object(plans, plan["phases"])
         if rank == 0:
             got = stencil.combine_memory(tiles, PX, PY)
-            q.put((all(i == ids[0] for i in ids) and len(ids[0]) == 128, all(p == plans[0] for p in plans),
+            q.put((all(i == ids[0] for i in ids) and len(ids[0]) == 128 and no_gpu_fails,
+                   all(p == plans[0] for p in plans),
                    bool(np.array_equal(got.view(np.uint32), o.stencil(g, T).view(np.uint32)))))
     finally:
         dist.destroy_process_group()
@@ -234,6 +244,6 @@ def test_gloo_world2_halo_protocol(pxpy, T):
         p.join(timeout=240)
         assert p.exitcode == 0
     same_uid, same_plan, exact = q.get(timeout=5)
-    assert same_uid, "RCCL unique id not shared through the store"
+    assert same_uid, "RCCL unique id not shared through the store (or smi_init did not fail without a GPU)"
     assert same_plan, "ranks planned different phases"
     assert exact, "decomposed depth-K halo protocol differs from the single-grid oracle"
