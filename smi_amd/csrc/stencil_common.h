@@ -120,6 +120,10 @@ struct SweepKArgs {
     int gT, gB, gL, gR;
 };
 constexpr int SWEEPK_MIN = 3, SWEEPK_MAX = 12;
+// Lanes per 64-lane window side that never store (the window apron is 4x
+// as many columns, >= K): 4 for K >= 9 (224 stored columns, line-aligned
+// stores), else the minimal ceil(K / 4).
+__host__ __device__ constexpr int sweepk_apron_lanes(int K) { return K >= 9 ? 4 : (K + 3) / 4; }
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s);
 int sweepk_window_cols(int K);  // output columns per 256-column window
 

@@ -33,7 +33,7 @@ static int resident_waves(int K) {
     }
 }
 
-int sweepk_window_cols(int K) { return 256 - 8 * ((K + 3) / 4); }
+int sweepk_window_cols(int K) { return 256 - 8 * sweepk_apron_lanes(K); }
 
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
     if (a.row_hi <= a.row_lo || a.col_hi <= a.col_lo) return SMI_SUCCESS;

@@ -27,21 +27,10 @@
 // single-tile sweep (whole tile) and, in multi-rank runs, the interior sweep
 // that stays K rows / KC columns clear of every halo-facing side.
 //
-// Window apron: K >= 9 uses 16 columns (4 lanes) per side, so a window
-// stores 224 columns = 7 whole 128-byte lines at a line-aligned offset
-// (strip starts are multiples of 224 columns); smaller K keep the minimal
-// float4 apron.  Round 2 (tools/sweepbench, 8192^2, K=12, ping-pong): the
-// aligned apron + the pre-loop drain + the batch issue barrier run a pass in
-// 0.117 ms vs 0.122 ms; the same grid streaming its loads and stores with no
-// levels takes 0.106 ms and the levels alone (cache-resident inputs) 0.094
-// ms, so the pass is now within ~10 % of its memory floor for this traffic
-// (594 MB, 1.1x the 537 MB minimum: window and row-block aprons).
-//
 // Measured alternative (round 2, tools/sweepbench): an LDS-DMA input ring
 // with hand-placed vmcnt waits and independent level groups reached 3
 // waves/SIMD at 145 VGPRs but ran 0.129 ms per 12-step pass at 8192^2 vs
-// 0.110 ms for this kernel in the same harness (2 waves/SIMD; single-buffer
-// timing): the per-step ds_read + sched barriers turned
+// 0.110 ms here (2 waves/SIMD): the per-step ds_read + sched barriers turned
 // the pass issue-stall bound (SQ_WAIT_INST_ANY 2.7x, VALU instructions 1.23x;
 // profiles/r02/).
 #pragma once
@@ -95,14 +84,34 @@ __device__ __forceinline__ void static_for(F &&f) {
 // strip holding column 0, bit 1 for the one holding column Y-1 (both only
 // when one window spans the whole tile); every other wave runs the plain
 // 12-instruction step.
-enum { ROW_NONE = 0, ROW_TOP = 1, ROW_BOT = 2, ROW_FULL = 3 };
+enum { ROW_NONE = 0, ROW_TOP = 1, ROW_BOT = 2, ROW_FULL = 3, ROW_UP = 4 };  // ROW_UP: ROW_NONE walking upwards
+template <int ROW> constexpr bool walks_up() { return ROW == ROW_BOT || ROW == ROW_UP; }
+__host__ __device__ constexpr bool walks_up_rt(int row) { return row == ROW_BOT || row == ROW_UP; }
 
 template <int K, int U>
 struct SweepK {
     static_assert(K >= SWEEPK_MIN && K <= SWEEPK_MAX, "3 <= K <= 12");
     static_assert(U % 3 == 0, "batch must be a multiple of the 3-slot ring");
-    static constexpr int LL = sweepk_apron_lanes(K);  // lanes per window side that never store
-    static constexpr int KC = 4 * LL;                  // window apron in columns (>= K)
+#ifndef SB_LL
+#define SB_LL(K) (((K) + 3) / 4)
+#endif
+#ifndef SB_COMPUTE_ONLY
+#define SB_COMPUTE_ONLY 0
+#endif
+#ifndef SB_MEM_ONLY
+#define SB_MEM_ONLY 0
+#endif
+#ifndef SB_LDS_PAD
+#define SB_LDS_PAD 0
+#endif
+#ifndef SB_ASM_STORE
+#define SB_ASM_STORE 0
+#endif
+#ifndef SB_STORE_AUX
+#define SB_STORE_AUX 2
+#endif
+    static constexpr int LL = SB_LL(K);  // lanes per window side that never store
+    static constexpr int KC = 4 * LL;       // window apron in columns (>= K)
     static constexpr int PRO = 2 * K + 1;   // prologue input rows (the last one stores the first output row)
 
     const float *__restrict__ in;
@@ -118,7 +127,11 @@ struct SweepK {
 
     template <bool REV>
     __device__ __forceinline__ float4 ld(int t) const {
+#if SB_COMPUTE_ONLY
+        const int r = (REV ? r_begin - t : r_begin + t) & 3;  // 4 rows: cache hits
+#else
         const int r = min(max(REV ? r_begin - t : r_begin + t, 0), rows - 1);
+#endif
         return *reinterpret_cast<const float4 *>(in + (size_t)r * cols + cl);
     }
 
@@ -159,7 +172,7 @@ struct SweepK {
     // row (N) and input t the lower (S); walking up they swap.
     template <int ROW, int CE, int PH>
     __device__ __forceinline__ float4 level(int l, int t, const float4 (&P)[3]) const {
-        if constexpr (ROW == ROW_BOT)
+        if constexpr (walks_up<ROW>())
             return step<ROW, CE>(r_begin - (t - l), P[PH], P[(PH + 2) % 3], P[(PH + 1) % 3]);
         else
             return step<ROW, CE>(r_begin + t - l, P[(PH + 1) % 3], P[(PH + 2) % 3], P[PH]);
@@ -168,6 +181,10 @@ struct SweepK {
     // Input row t arrives with value x; PH = t mod 3.
     template <int ROW, int CE, int PH>
     __device__ __forceinline__ void advance(int t, const float4 &x) {
+#if SB_MEM_ONLY
+        store_row<walks_up<ROW>()>(t, x);  // stream only: the same loads and stores, no levels
+        return;
+#endif
         W[0][PH] = x;
         float4 v;
         static_for<K>([&](auto L) {
@@ -175,7 +192,7 @@ struct SweepK {
             v = level<ROW, CE, PH>(l, t, W[l - 1]);
             if constexpr (l < K) W[l][PH] = v;
         });
-        store_row<ROW == ROW_BOT>(t, v);
+        store_row<walks_up<ROW>()>(t, v);
     }
 
     // Branch-free predicated store of the level-K row produced by input t:
@@ -189,17 +206,29 @@ struct SweepK {
         const int j = REV ? o1 - 1 - (t - 2 * K) : o0 + (t - 2 * K);
         const bool in_block = REV ? j >= o0 : j < o1;
         const int jj = __builtin_amdgcn_readfirstlane(min(max(j, 0), rows - 1));
-        const int nrec = __builtin_amdgcn_readfirstlane(in_block ? row_bytes : 0);
-        __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(out + (size_t)jj * cols, (short)0, nrec, 0x00020000);
+        const int nrec = __builtin_amdgcn_readfirstlane(in_block && !SB_COMPUTE_ONLY ? row_bytes : 0);
         const u32x4 d = {__builtin_bit_cast(unsigned int, v.x), __builtin_bit_cast(unsigned int, v.y),
                          __builtin_bit_cast(unsigned int, v.z), __builtin_bit_cast(unsigned int, v.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(d, rs, voff, 0, 2 /* nt */);
+#if SB_ASM_STORE
+        // the store as inline asm: the compiler's wait-count pass does not
+        // see it, so no later s_waitcnt waits for a store to complete; the
+        // s_nop covers the VALU-overwrites-store-data hazard
+        const unsigned long long base = (unsigned long long)(out + (size_t)jj * cols);
+        const u32x4 rsrc = {(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)base),
+                            (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(base >> 32)) & 0xffffu,
+                            (unsigned)nrec, 0x00020000u};
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen nt\n\ts_nop 1" ::"v"(d), "v"(voff), "s"(rsrc)
+                     : "memory");
+#else
+        __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(out + (size_t)jj * cols, (short)0, nrec, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(d, rs, voff, 0, SB_STORE_AUX);
+#endif
     }
 
     template <int ROW, int CE>
     __device__ __forceinline__ void run() {
-        constexpr bool REV = ROW == ROW_BOT;
+        constexpr bool REV = walks_up<ROW>();
         // prologue: input rows 0 .. 2K, compile-time indices; level l starts
         // at input 2l (the first row it must produce)
         static_for<PRO>([&](auto T) {
@@ -217,21 +246,36 @@ struct SweepK {
             });
             if constexpr (t == 2 * K) store_row<REV>(t, v);
         });
-        // steady state: 2U input rows per iteration, loads one batch ahead
+        // steady state (experiment switches: SB_AHEAD batches of loads in
+        // flight, SB_PIN = scheduling barrier after every load batch)
         const int n_in = (o1 - o0) + 2 * K;
+#ifndef SB_AHEAD
+#define SB_AHEAD 1
+#endif
+#ifndef SB_PIN
+#define SB_PIN 0
+#endif
+#if SB_PIN
+#define SB_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SB_BARRIER() (void)0
+#endif
+#ifndef SB_DRAIN
+#define SB_DRAIN 0
+#endif
+#if SB_AHEAD == 1
         float4 A[U], B[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) A[u] = ld<REV>(PRO + u);
-        // Drain before the loop.  Without it the wait-count pass merges the
-        // loads pending from the prologue into the loop header's state and
-        // waits there for the store issued a few instructions earlier (a full
-        // store round trip per iteration); with it every wait in the loop
-        // targets a load or store issued >= 2 rows of work before.
+#if SB_DRAIN
+        // drain before the loop: the wait-count pass then sees nothing
+        // pending from the preheader at the loop header, only the back edge
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+#endif
         for (int t = PRO; t < n_in; t += 2 * U) {
 #pragma unroll
             for (int u = 0; u < U; ++u) B[u] = ld<REV>(t + U + u);
-            __builtin_amdgcn_sched_barrier(0);  // issue the batch here, a whole batch ahead of its use
+            SB_BARRIER();
             static_for<U>([&](auto V) {
                 constexpr int ph = (PRO + V) % 3;
                 advance<ROW, CE, ph>(t + V, A[V]);
@@ -239,19 +283,61 @@ struct SweepK {
             if (t + U >= n_in) break;  // uniform
 #pragma unroll
             for (int u = 0; u < U; ++u) A[u] = ld<REV>(t + 2 * U + u);
-            __builtin_amdgcn_sched_barrier(0);
+            SB_BARRIER();
             static_for<U>([&](auto V) {
                 constexpr int ph = (PRO + U + V) % 3;
                 advance<ROW, CE, ph>(t + U + V, B[V]);
             });
         }
+#else
+        float4 A[U], B[U], C[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) A[u] = ld<REV>(PRO + u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) B[u] = ld<REV>(PRO + U + u);
+#if SB_DRAIN
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+#endif
+        for (int t = PRO; t < n_in; t += 3 * U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) C[u] = ld<REV>(t + 2 * U + u);
+            SB_BARRIER();
+            static_for<U>([&](auto V) {
+                constexpr int ph = (PRO + V) % 3;
+                advance<ROW, CE, ph>(t + V, A[V]);
+            });
+            if (t + U >= n_in) break;  // uniform
+#pragma unroll
+            for (int u = 0; u < U; ++u) A[u] = ld<REV>(t + 3 * U + u);
+            SB_BARRIER();
+            static_for<U>([&](auto V) {
+                constexpr int ph = (PRO + U + V) % 3;
+                advance<ROW, CE, ph>(t + U + V, B[V]);
+            });
+            if (t + 2 * U >= n_in) break;  // uniform
+#pragma unroll
+            for (int u = 0; u < U; ++u) B[u] = ld<REV>(t + 4 * U + u);
+            SB_BARRIER();
+            static_for<U>([&](auto V) {
+                constexpr int ph = (PRO + 2 * U + V) % 3;
+                advance<ROW, CE, ph>(t + 2 * U + V, C[V]);
+            });
+        }
+#endif
     }
 };
 
 template <int K>
-__global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, int nrb) {
+#ifndef SB_WPE
+#define SB_WPE 1
+#endif
+__global__ __launch_bounds__(256, SB_WPE) void sweepk_kernel(SweepKArgs a, int nstrips, int nrb) {
     using S = SweepK<K, 3>;
     constexpr int SW = 256 - 2 * S::KC;  // output columns per window
+#if SB_LDS_PAD
+    __shared__ float pad[SB_LDS_PAD / 4];  // occupancy limiter for timing experiments
+    if (threadIdx.x == 1000) pad[a.rows & 7] = 0.f;
+#endif
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
     const int task = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
@@ -289,7 +375,14 @@ __global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, 
         row = ROW_BOT;
     else if (touchT || touchB)
         row = ROW_FULL;
-    w.r_begin = row == ROW_BOT ? w.o1 - 1 + K : w.o0 - K;
+#ifndef SB_ALT
+#define SB_ALT 0
+#endif
+    // alternate walk directions: the boundary rows of two adjacent row
+    // blocks are then read by both waves at the same time (the start or the
+    // end of both walks), so the second read of each apron hits L2
+    if (SB_ALT && row == ROW_NONE && (rb & 1)) row = ROW_UP;
+    w.r_begin = walks_up_rt(row) ? w.o1 - 1 + K : w.o0 - K;
     switch (row * 4 + ce) {
     case 0: w.template run<ROW_NONE, 0>(); break;
     case 1: w.template run<ROW_NONE, 1>(); break;
@@ -303,6 +396,12 @@ __global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, 
     case 9: w.template run<ROW_BOT, 1>(); break;
     case 10: w.template run<ROW_BOT, 2>(); break;
     case 11: w.template run<ROW_BOT, 3>(); break;
+#if SB_ALT
+    case 16: w.template run<ROW_UP, 0>(); break;
+    case 17: w.template run<ROW_UP, 1>(); break;
+    case 18: w.template run<ROW_UP, 2>(); break;
+    case 19: w.template run<ROW_UP, 3>(); break;
+#endif
     default: w.template run<ROW_FULL, 3>(); break;
     }
 }

@@ -79,7 +79,7 @@ int main(int argc, char **argv) {
     CK(hipDeviceSynchronize());
 
     smi::SweepKArgs args{a, b, n, n, 0, n, 0, n, 1, 1, 1, 1};
-    constexpr int KC = 4 * ((K + 3) / 4);
+    constexpr int KC = smi::SweepK<K, 3>::KC;
     const int sw = 256 - 2 * KC;
     int per_cu = 0, cus = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, smi::sweepk_kernel<K>, 256, 0));
@@ -92,10 +92,22 @@ int main(int argc, char **argv) {
         const int per_strip = std::max(1, waves / nstrips);
         ht = std::max(2 * K, (out_rows + per_strip - 1) / per_strip);
     }
-    const int nrb = (out_rows + ht - 1) / ht;
+    int nrb = (out_rows + ht - 1) / ht;
+#ifdef SB_EVEN_NRB
+    nrb += nrb & 1;  // alternating walks: first block down, last block up
+#endif
     const int blocks = (int)(((long)nstrips * nrb + 3) / 4);
+    // timing ping-pongs between the two buffers like a real run (reading the
+    // same input every launch would let the 256 MB MALL hold part of it)
+    bool flip = false;
     auto launch = [&]() {
-        hipLaunchKernelGGL((smi::sweepk_kernel<K>), dim3(blocks), dim3(256), 0, 0, args, nstrips, nrb);
+        smi::SweepKArgs la = args;
+        if (flip) {
+            la.in = args.out;
+            la.out = const_cast<float *>(args.in);
+        }
+        flip = !flip;
+        hipLaunchKernelGGL((smi::sweepk_kernel<K>), dim3(blocks), dim3(256), 0, 0, la, nstrips, nrb);
     };
     launch();
     CK(hipDeviceSynchronize());
