@@ -301,17 +301,23 @@ int smi_reduce(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count, 
     const size_t cs = chunk_elems(count, n, esz);
     const size_t my_len = chunk_len(count, cs, me);
     const Pieces pc = pieces_of(cs, esz);
-    // workspace: two exchange slots of n x ps staging elements, plus the
-    // reduced chunk of a non-root owner (cs elements)
+    // workspace: two exchange slots of n staging rows, plus the reduced
+    // chunk of a non-root owner (cs elements).  Rows sit kStagePad bytes
+    // further apart than a piece: with power-of-two row strides the fold's
+    // n concurrent row streams collide in the same HBM channels (8 x 64 Mi
+    // fp32 fold: 0.72 of HBM peak at a 256 MiB row stride, 0.80 with 4 KiB
+    // more, profiles/r02/fold_stride.jsonl).
+    constexpr size_t kStagePad = 4096;
+    const size_t pst = pc.ps + kStagePad / esz;  // staging row stride in elements
     void *ws = nullptr;
-    SMI_TRY(comm_workspace(c, (2 * (size_t)n * pc.ps + cs) * esz, &ws));
+    SMI_TRY(comm_workspace(c, (2 * (size_t)n * pst + cs) * esz, &ws));
     char *stage = (char *)ws;
-    char *mine = stage + 2 * (size_t)n * pc.ps * esz;
+    char *mine = stage + 2 * (size_t)n * pst * esz;
     const char *sb = (const char *)sendbuf;
     char *dst = (me == root) ? (char *)recvbuf + (size_t)me * cs * esz : mine;
     Transport *tp = c->transport.get();
     hipStream_t cs_ = c->comm_stream;
-    auto slot = [&](int i, int k) { return stage + ((size_t)(i & 1) * n + k) * pc.ps * esz; };
+    auto slot = [&](int i, int k) { return stage + ((size_t)(i & 1) * n + k) * pst * esz; };
     auto sub = [&](int owner, int i) { return sub_len(chunk_len(count, cs, owner), pc.ps, i); };
 
     // Pipelined over P pieces (every owner chunk split into P sub-chunks of

@@ -20,6 +20,7 @@
 // fold consumes the slab's tiles in order from lane 0 (readlane), so no tile
 // array is kept and m is unbounded.
 #include <algorithm>
+#include <cstdlib>
 
 #include "smi_internal.h"
 
@@ -48,34 +49,88 @@ __device__ __forceinline__ float4 ld_stream(const float *p) {
 }
 
 constexpr int kGemvWaves = 4;
-constexpr int kSlabStride = 17;  // float4s per chunk in LDS (64 floats + 4 pad: conflict-free)
 
-// c for the chunk this lane owns: products of slab `pv` (coalesced layout:
-// pv[j] = elements 4*(64j + lane) .. +3 of the slab) transposed through `wb`.
-__device__ __forceinline__ float chunk_sum(float4 *wb, const float4 (&pv)[16], int lane) {
+// c for the chunk this lane owns, continued over one pass of a slab: `pv`
+// holds the pass's products in the coalesced layout (load j = chunks
+// CPL*j .. CPL*j + CPL-1 of the slab, LPC lanes x float4 each) and is
+// transposed through `wb` so that lane l sums chunk l's 64/H elements of this
+// pass in order, continuing `c` (the reference's sequential chunk sum,
+// gesummv_rank0.cl:137-149).
+template <int H>
+struct SlabPass {
+    static constexpr int J = 16 / H;       // float4 loads per matrix per lane and pass
+    static constexpr int LPC = 16 / H;     // lanes per chunk in a load
+    static constexpr int CPL = 64 / LPC;   // chunks per load instruction
+    static constexpr int SS = LPC + 1;     // float4 stride of a chunk in LDS (+1 pad: conflict-free)
+    static constexpr int LDS_F4 = 64 * SS; // per wave
+};
+
+template <int H>
+__device__ __forceinline__ float chunk_sum(float4 *wb, const float4 (&pv)[SlabPass<H>::J], int lane, float c) {
+    using P = SlabPass<H>;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) wb[(4 * j + (lane >> 4)) * kSlabStride + (lane & 15)] = pv[j];
+    for (int j = 0; j < P::J; ++j) wb[(P::CPL * j + lane / P::LPC) * P::SS + (lane % P::LPC)] = pv[j];
     wave_lds_sync();
-    float c = 0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const float4 p = wb[lane * kSlabStride + q];
+    for (int q = 0; q < P::LPC; ++q) {
+        const float4 p = wb[lane * P::SS + q];
         c = __fadd_rn(c, p.x);
         c = __fadd_rn(c, p.y);
         c = __fadd_rn(c, p.z);
         c = __fadd_rn(c, p.w);
     }
-    wave_lds_sync();  // reads done before the next slab overwrites
+    wave_lds_sync();  // reads done before the next pass overwrites
     return c;
 }
 
+// Tile values of one slab (64 chunks = 32 tiles from chunk cbase on), read
+// in H passes of 64/H elements per chunk: tile k of the slab ends up in lane
+// 2k of tA (and tB), in the reference's per-tile order
+// acc_t = (0 + alpha*c_{2t}) + alpha*c_{2t+1} (gesummv_rank0.cl:111,158);
+// a chunk past the row's end counts as c = 0.
+template <bool HAS_B, int H>
+__device__ __forceinline__ void slab_tiles(const float *a, const float *b, const float *x, float4 *wb, int cbase,
+                                           int nchunks, int lane, float alpha, float beta, float &tA, float &tB) {
+    using P = SlabPass<H>;
+    float cA = 0.f, cB = 0.f;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+        float4 pa[P::J], pb[P::J];
+#pragma unroll
+        for (int j = 0; j < P::J; ++j) {
+            const int ch = min(cbase + P::CPL * j + lane / P::LPC, nchunks - 1);  // clamped: the tail
+            const int e = ch * 64 + h * (64 / H) + (lane % P::LPC) * 4;            // chunk's c is replaced
+            const float4 xv = *reinterpret_cast<const float4 *>(x + e);
+            pa[j] = mul4(ld_stream(a + e), xv);  // A, B streamed once; x stays cached
+            if constexpr (HAS_B) pb[j] = mul4(ld_stream(b + e), xv);
+        }
+        // every lane writes slots of other lanes' chunks: transpose on all lanes
+        cA = chunk_sum<H>(wb, pa, lane, cA);
+        if constexpr (HAS_B) cB = chunk_sum<H>(wb, pb, lane, cB);
+    }
+    const bool valid = cbase + lane < nchunks;  // replace a missing chunk's c by +0
+    cA = valid ? cA : 0.f;
+    const float nA = dpp_from_next(cA);
+    tA = __fadd_rn(__fadd_rn(0.f, __fmul_rn(alpha, cA)), __fmul_rn(alpha, nA));
+    tB = 0.f;
+    if constexpr (HAS_B) {
+        cB = valid ? cB : 0.f;
+        const float nB = dpp_from_next(cB);
+        tB = __fadd_rn(__fadd_rn(0.f, __fmul_rn(beta, cB)), __fmul_rn(beta, nB));
+    }
+}
+
+// One wave per row: the slabs are walked in order and each slab's tiles are
+// folded into the row sum straight from the even lanes (readlane), so no
+// tile array is kept and m is unbounded.  Used for rows longer than
+// kSplitMaxCols.
 template <bool HAS_B>
 __global__ __launch_bounds__(64 * kGemvWaves) void gemv_rows_kernel(const float *__restrict__ A,
                                                                    const float *__restrict__ B,
                                                                    const float *__restrict__ x,
                                                                    float *__restrict__ y, int n, int m, int lda,
                                                                    float alpha, float beta) {
-    __shared__ float4 lds[kGemvWaves][64 * kSlabStride];
+    __shared__ float4 lds[kGemvWaves][SlabPass<1>::LDS_F4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int row = blockIdx.x * kGemvWaves + wave;
     if (row >= n) return;  // wave-uniform; the kernel has no block barrier
@@ -85,29 +140,8 @@ __global__ __launch_bounds__(64 * kGemvWaves) void gemv_rows_kernel(const float 
     const float *b = HAS_B ? B + (size_t)row * lda : a;
     float accA = 0.f, accB = 0.f;
     for (int cbase = 0; cbase < nchunks; cbase += 64) {
-        float4 pa[16], pb[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int ch = min(cbase + 4 * j + (lane >> 4), nchunks - 1);  // clamped: the tail
-            const int e = ch * 64 + (lane & 15) * 4;                       // chunk's c is replaced
-            const float4 xv = *reinterpret_cast<const float4 *>(x + e);
-            pa[j] = mul4(ld_stream(a + e), xv);  // A, B streamed once; x stays cached
-            if constexpr (HAS_B) pb[j] = mul4(ld_stream(b + e), xv);
-        }
-        const bool valid = cbase + lane < nchunks;
-        // every lane writes slots of other lanes' chunks: transpose on all
-        // lanes, then replace a missing chunk's c by +0
-        float cA = chunk_sum(wb, pa, lane);
-        cA = valid ? cA : 0.f;
-        const float nA = dpp_from_next(cA);
-        const float tA = __fadd_rn(__fadd_rn(0.f, __fmul_rn(alpha, cA)), __fmul_rn(alpha, nA));
-        float tB = 0.f;
-        if constexpr (HAS_B) {
-            float cB = chunk_sum(wb, pb, lane);
-            cB = valid ? cB : 0.f;
-            const float nB = dpp_from_next(cB);
-            tB = __fadd_rn(__fadd_rn(0.f, __fmul_rn(beta, cB)), __fmul_rn(beta, nB));
-        }
+        float tA, tB;
+        slab_tiles<HAS_B, 1>(a, b, x, wb, cbase, nchunks, lane, alpha, beta, tA, tB);
         // tiles of this slab live in the even lanes, in order
         const int ntl = min(32, (nchunks - cbase + 1) >> 1);
         for (int k = 0; k < ntl; ++k) {
@@ -121,12 +155,96 @@ __global__ __launch_bounds__(64 * kGemvWaves) void gemv_rows_kernel(const float 
     if (lane == 0) y[row] = HAS_B ? __fadd_rn(accA, accB) : accA;
 }
 
+// Row split over the workgroup's waves (rows up to kSplitMaxCols): wave w
+// computes slabs w, w + 4, ... and parks their tile values in LDS at their
+// place in the row; after one barrier wave 0 folds the row's tiles in order.
+// A workgroup is a quarter of the old one-wave-per-row work unit, so the
+// grid has 4x the units: a 4096-row shard (BASELINE config 5 per GPU) is
+// 8 rounds of resident workgroups instead of 2, and no CU idles through a
+// long last round.  The tile values and the fold order are those of
+// gemv_rows_kernel, so the two are bit-identical.
+constexpr int kSplitMaxCols = 32768;  // 2 KiB of tiles: 4 workgroups of 4 waves fill a CU's LDS
+constexpr int kSplitMaxTiles = kSplitMaxCols / 128;
+template <bool HAS_B, int H>
+__global__ __launch_bounds__(64 * kGemvWaves) void gemv_split_kernel(const float *__restrict__ A,
+                                                                    const float *__restrict__ B,
+                                                                    const float *__restrict__ x,
+                                                                    float *__restrict__ y, int n, int m, int lda,
+                                                                    float alpha, float beta) {
+    __shared__ float4 lds[kGemvWaves][SlabPass<H>::LDS_F4];
+    __shared__ __attribute__((aligned(16))) float tiles[2][kSplitMaxTiles];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x;
+    float4 *wb = lds[wave];
+    const int nchunks = m >> 6;
+    const float *a = A + (size_t)row * lda;
+    const float *b = HAS_B ? B + (size_t)row * lda : a;
+    for (int s = wave; s * 64 < nchunks; s += kGemvWaves) {
+        float tA, tB;
+        slab_tiles<HAS_B, H>(a, b, x, wb, s * 64, nchunks, lane, alpha, beta, tA, tB);
+        // tile k of slab s -> tiles[s*32 + k]; missing tiles of the last
+        // slab read +0 (acc is never -0, so + 0 leaves it unchanged)
+        const int ntl = min(32, (nchunks - s * 64 + 1) >> 1);
+        if ((lane & 1) == 0) {
+            tiles[0][s * 32 + (lane >> 1)] = (lane >> 1) < ntl ? tA : 0.f;
+            if constexpr (HAS_B) tiles[1][s * 32 + (lane >> 1)] = (lane >> 1) < ntl ? tB : 0.f;
+        }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    const int nt4 = (((nchunks + 1) >> 1) + 3) >> 2;  // tiles, in float4 groups
+    const float4 *tA4 = reinterpret_cast<const float4 *>(tiles[0]);
+    const float4 *tB4 = reinterpret_cast<const float4 *>(tiles[1]);
+    float accA = 0.f, accB = 0.f;
+    for (int q = 0; q < nt4; ++q) {
+        const float4 ta = tA4[q];  // every lane reads the same address: broadcast
+        accA = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(accA, ta.x), ta.y), ta.z), ta.w);
+        if constexpr (HAS_B) {
+            const float4 tb = tB4[q];
+            accB = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(accB, tb.x), tb.y), tb.z), tb.w);
+        }
+    }
+    if (lane == 0) y[row] = HAS_B ? __fadd_rn(accA, accB) : accA;
+}
+
+// Launch variant (experiment switch SMI_GEMV_VARIANT; unset = 0, the default):
+// 1 = one wave per row for every shape; row split with 2 = whole-slab
+// passes, 3 = quarter-slab passes (default: half-slab passes).
+static int gemv_variant() {
+    static int v = [] {
+        const char *e = getenv("SMI_GEMV_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+template <int H>
+static void launch_split(const float *A, const float *B, const float *x, float *y, int n, int m, int lda,
+                         float alpha, float beta, hipStream_t s) {
+    if (B)
+        hipLaunchKernelGGL((gemv_split_kernel<true, H>), dim3(n), dim3(64 * kGemvWaves), 0, s, A, B, x, y, n, m, lda,
+                           alpha, beta);
+    else
+        hipLaunchKernelGGL((gemv_split_kernel<false, H>), dim3(n), dim3(64 * kGemvWaves), 0, s, A, B, x, y, n, m,
+                           lda, alpha, beta);
+}
+
 static int launch_gemv(const float *A, const float *B, const float *x, float *y, int n, int m, int lda,
                        float alpha, float beta, hipStream_t s) {
     if (n == 0) return SMI_SUCCESS;
     int tok = -1;
     if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_GEMV, s, &tok));
-    const dim3 grid((n + kGemvWaves - 1) / kGemvWaves), block(64 * kGemvWaves);
+    const dim3 block(64 * kGemvWaves);
+    if (m <= kSplitMaxCols && gemv_variant() != 1) {
+        const int v = gemv_variant();
+        if (v == 2) launch_split<1>(A, B, x, y, n, m, lda, alpha, beta, s);
+        else if (v == 3) launch_split<4>(A, B, x, y, n, m, lda, alpha, beta, s);
+        else launch_split<2>(A, B, x, y, n, m, lda, alpha, beta, s);
+        SMI_HIP_CHECK(hipGetLastError());
+        if (tok >= 0) SMI_TRY(prof_end(tok, s));
+        return SMI_SUCCESS;
+    }
+    const dim3 grid((n + kGemvWaves - 1) / kGemvWaves);
     if (B)
         hipLaunchKernelGGL(gemv_rows_kernel<true>, grid, block, 0, s, A, B, x, y, n, m, lda, alpha, beta);
     else
