@@ -44,11 +44,30 @@
 // timing): the per-step ds_read + sched barriers turned
 // the pass issue-stall bound (SQ_WAIT_INST_ANY 2.7x, VALU instructions 1.23x;
 // profiles/r02/).
+//
+// Scaled levels (round 2).  x 0.25 is a power-of-two scaling, and IEEE
+// round-to-nearest commutes with power-of-two scaling whenever nothing
+// overflows and no rounding happens in the subnormal range.  So level l can
+// carry u_l = 4^l v_l: u_l = ((S'+W')+E')+N' over the level-(l-1) values u,
+// with no multiply (copied edge cells: u_l = 4 u_{l-1}), and the store
+// writes u_K * 4^-K.  This is bit-identical to the reference arithmetic
+// when every finite nonzero input of the wave's cone has magnitude in
+// [2^-100, 2^101): then every level-l value is a multiple of 2^(-123-2l)
+// (>= 2^-147 for l <= 12, so each x 0.25 of the reference order is exact,
+// subnormal or not), and |u| < 2^(2K+101) <= 2^125 never overflows; Inf and
+// NaN propagate the same either way.  Each wave checks its inputs as they
+// stream in (frexp exponents) and a block that fails walks again with the
+// exact arithmetic.  The multiply was 2 of the 12 VALU instructions of a
+// level step (4 of 16.3 issue-slot units, packed ops at half rate).
 #pragma once
 
 #include <type_traits>
 
 #include "stencil_common.h"
+
+#ifndef SMI_SWEEPK_SCALED
+#define SMI_SWEEPK_SCALED 1
+#endif
 
 namespace smi {
 
@@ -104,6 +123,9 @@ struct SweepK {
     static constexpr int LL = sweepk_apron_lanes(K);  // lanes per window side that never store
     static constexpr int KC = 4 * LL;                  // window apron in columns (>= K)
     static constexpr int PRO = 2 * K + 1;   // prologue input rows (the last one stores the first output row)
+    static constexpr bool kScaled = SMI_SWEEPK_SCALED != 0;
+    static constexpr int kExpLo = -99, kExpHi = 101;      // frexp exponent range of the scaled walk's inputs
+    static constexpr float kUnscale = 1.0f / (float)(1u << (2 * K));  // 4^-K (exact: K <= 12)
 
     const float *__restrict__ in;
     float *__restrict__ out;
@@ -122,34 +144,48 @@ struct SweepK {
         return *reinterpret_cast<const float4 *>(in + (size_t)r * cols + cl);
     }
 
-    template <int ROW, int CE>
+    // One level step of 4 cells per lane.  SC (scaled): the operands carry
+    // 4^(l-1) times their level-(l-1) values, so the sum ((S+W)+E)+N is
+    // 4^l times the level-l value and the x 0.25 is skipped (copied edge
+    // cells are scaled by 4 instead); see "Scaled levels" above.
+    template <int ROW, int CE, bool SC>
     __device__ __forceinline__ float4 step(int i, const float4 &n, const float4 &c, const float4 &s) const {
         const float w = shr1_any(c.w);
         const float e = shl1_any(c.x);
-        // ((S + W) + E) element-wise, then (+ N) and (x 0.25) on packed
+        // ((S + W) + E) element-wise, then (+ N) (and x 0.25) on packed
         // pairs (v_pk_add_f32 / v_pk_mul_f32: same IEEE single-precision
         // round-to-nearest results as the scalar ops, never contracted)
-        f32x2 sw01 = {__fadd_rn(s.x, w), __fadd_rn(s.y, c.x)};
-        f32x2 sw23 = {__fadd_rn(s.z, c.y), __fadd_rn(s.w, c.z)};
-        f32x2 swe01 = {__fadd_rn(sw01.x, c.y), __fadd_rn(sw01.y, c.z)};
-        f32x2 swe23 = {__fadd_rn(sw23.x, c.w), __fadd_rn(sw23.y, e)};
-        const f32x2 q = {0.25f, 0.25f};
-        const f32x2 o01 = (swe01 + f32x2{n.x, n.y}) * q;
-        const f32x2 o23 = (swe23 + f32x2{n.z, n.w}) * q;
+        float b0 = __fadd_rn(__fadd_rn(s.x, w), c.y);
+        float b1 = __fadd_rn(__fadd_rn(s.y, c.x), c.z);
+        float b2 = __fadd_rn(__fadd_rn(s.z, c.y), c.w);
+        float b3 = __fadd_rn(__fadd_rn(s.w, c.z), e);
+        if constexpr (SC) {
+            // opaque: keeps the instruction selector from re-pairing the
+            // scalar adds into v_pk_add_f32 with register moves for operands
+            asm("" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+        }
+        f32x2 o01 = f32x2{b0, b1} + f32x2{n.x, n.y};
+        f32x2 o23 = f32x2{b2, b3} + f32x2{n.z, n.w};
+        if constexpr (!SC) {
+            const f32x2 q = {0.25f, 0.25f};
+            o01 = o01 * q;
+            o23 = o23 * q;
+        }
         float4 o;
         o.x = o01.x;
         o.y = o01.y;
         o.z = o23.x;
         o.w = o23.y;
         if constexpr (ROW == ROW_FULL) {
+            static_assert(!SC, "ROW_FULL blocks run the exact arithmetic only");
             const bool rcopy = (i == 0 && gT) || (i == rows - 1 && gB);
             o.x = (rcopy || copyL) ? c.x : o.x;
             o.y = rcopy ? c.y : o.y;
             o.z = rcopy ? c.z : o.z;
             o.w = (rcopy || copyR) ? c.w : o.w;
         } else {
-            if constexpr (CE & 1) o.x = copyL ? c.x : o.x;
-            if constexpr (CE & 2) o.w = copyR ? c.w : o.w;
+            if constexpr (CE & 1) o.x = copyL ? (SC ? c.x * 4.0f : c.x) : o.x;
+            if constexpr (CE & 2) o.w = copyR ? (SC ? c.w * 4.0f : c.w) : o.w;
         }
         return o;
     }
@@ -157,25 +193,39 @@ struct SweepK {
     // level l (1..K) at input t from the level l-1 rows of inputs t-2, t-1, t
     // (slots PH+1, PH+2, PH mod 3).  Walking down, input t-2 is the upper
     // row (N) and input t the lower (S); walking up they swap.
-    template <int ROW, int CE, int PH>
+    template <int ROW, int CE, bool SC, int PH>
     __device__ __forceinline__ float4 level(int l, int t, const float4 (&P)[3]) const {
         if constexpr (ROW == ROW_BOT)
-            return step<ROW, CE>(r_begin - (t - l), P[PH], P[(PH + 2) % 3], P[(PH + 1) % 3]);
+            return step<ROW, CE, SC>(r_begin - (t - l), P[PH], P[(PH + 2) % 3], P[(PH + 1) % 3]);
         else
-            return step<ROW, CE>(r_begin + t - l, P[(PH + 1) % 3], P[(PH + 2) % 3], P[PH]);
+            return step<ROW, CE, SC>(r_begin + t - l, P[(PH + 1) % 3], P[(PH + 2) % 3], P[PH]);
+    }
+
+    // Scaled-path guard: frexp exponents of every input the wave consumes
+    // (0 for zeros, Inf and NaN); the scaled levels are exact when every one
+    // lies in [-99, 101] (finite nonzero magnitudes in [2^-100, 2^101)).
+    int emin, emax;
+    __device__ __forceinline__ void note(const float4 &x) {
+        const int e0 = __builtin_amdgcn_frexp_expf(x.x), e1 = __builtin_amdgcn_frexp_expf(x.y);
+        const int e2 = __builtin_amdgcn_frexp_expf(x.z), e3 = __builtin_amdgcn_frexp_expf(x.w);
+        emin = min(emin, min(e0, e1));
+        emax = max(emax, max(e0, e1));
+        emin = min(emin, min(e2, e3));
+        emax = max(emax, max(e2, e3));
     }
 
     // Input row t arrives with value x; PH = t mod 3.
-    template <int ROW, int CE, int PH>
+    template <int ROW, int CE, bool SC, int PH>
     __device__ __forceinline__ void advance(int t, const float4 &x) {
         W[0][PH] = x;
+        if constexpr (SC) note(x);
         float4 v;
         static_for<K>([&](auto L) {
             constexpr int l = L + 1;
-            v = level<ROW, CE, PH>(l, t, W[l - 1]);
+            v = level<ROW, CE, SC, PH>(l, t, W[l - 1]);
             if constexpr (l < K) W[l][PH] = v;
         });
-        store_row<ROW == ROW_BOT>(t, v);
+        store_row<ROW == ROW_BOT, SC>(t, v);
     }
 
     // Branch-free predicated store of the level-K row produced by input t:
@@ -184,8 +234,14 @@ struct SweepK {
     // carry an offset beyond it and the hardware range check drops them.  No
     // branch splits the unrolled rows, so the scheduler interleaves their
     // dependency chains.  Nontemporal: the output is not re-read this pass.
-    template <bool REV>
-    __device__ __forceinline__ void store_row(int t, const float4 &v) const {
+    template <bool REV, bool SC>
+    __device__ __forceinline__ void store_row(int t, const float4 &vs) const {
+        float4 v = vs;
+        if constexpr (SC) {  // 4^K u -> u: exact (see "Scaled levels")
+            const f32x2 q = {kUnscale, kUnscale};
+            const f32x2 a = f32x2{vs.x, vs.y} * q, b = f32x2{vs.z, vs.w} * q;
+            v = make_float4(a.x, a.y, b.x, b.y);
+        }
         const int j = REV ? o1 - 1 - (t - 2 * K) : o0 + (t - 2 * K);
         const bool in_block = REV ? j >= o0 : j < o1;
         const int jj = __builtin_amdgcn_readfirstlane(min(max(j, 0), rows - 1));
@@ -197,25 +253,34 @@ struct SweepK {
         __builtin_amdgcn_raw_buffer_store_b128(d, rs, voff, 0, 2 /* nt */);
     }
 
-    template <int ROW, int CE>
-    __device__ __forceinline__ void run() {
+    // Walks the block; returns false (wave-uniform) when SC and some input
+    // left the range where the scaled levels are exact -- the caller then
+    // walks the block again with SC = false.
+    template <int ROW, int CE, bool SC>
+    __device__ __forceinline__ bool run() {
         constexpr bool REV = ROW == ROW_BOT;
+        emin = 0;
+        emax = 0;
         // prologue: input rows 0 .. 2K, compile-time indices; level l starts
         // at input 2l (the first row it must produce)
         static_for<PRO>([&](auto T) {
             constexpr int t = T;
             W[0][t % 3] = ld<REV>(t);
+            if constexpr (SC) note(W[0][t % 3]);
             float4 v;
             static_for<K>([&](auto L) {
                 constexpr int l = L + 1;
                 if constexpr (t >= 2 * l) {
-                    v = level<ROW, CE, t % 3>(l, t, W[l - 1]);
+                    v = level<ROW, CE, SC, t % 3>(l, t, W[l - 1]);
                     // the edge row (0 walking down, X-1 walking up) is input t - l == K
-                    if constexpr ((ROW == ROW_TOP || ROW == ROW_BOT) && t - l == K) v = W[l - 1][(t + 2) % 3];
+                    if constexpr ((ROW == ROW_TOP || ROW == ROW_BOT) && t - l == K) {
+                        v = W[l - 1][(t + 2) % 3];
+                        if constexpr (SC) v = make_float4(v.x * 4.0f, v.y * 4.0f, v.z * 4.0f, v.w * 4.0f);
+                    }
                     if constexpr (l < K) W[l][t % 3] = v;
                 }
             });
-            if constexpr (t == 2 * K) store_row<REV>(t, v);
+            if constexpr (t == 2 * K) store_row<REV, SC>(t, v);
         });
         // steady state: 2U input rows per iteration, loads one batch ahead
         const int n_in = (o1 - o0) + 2 * K;
@@ -234,7 +299,7 @@ struct SweepK {
             __builtin_amdgcn_sched_barrier(0);  // issue the batch here, a whole batch ahead of its use
             static_for<U>([&](auto V) {
                 constexpr int ph = (PRO + V) % 3;
-                advance<ROW, CE, ph>(t + V, A[V]);
+                advance<ROW, CE, SC, ph>(t + V, A[V]);
             });
             if (t + U >= n_in) break;  // uniform
 #pragma unroll
@@ -242,9 +307,29 @@ struct SweepK {
             __builtin_amdgcn_sched_barrier(0);
             static_for<U>([&](auto V) {
                 constexpr int ph = (PRO + U + V) % 3;
-                advance<ROW, CE, ph>(t + U + V, B[V]);
+                advance<ROW, CE, SC, ph>(t + U + V, B[V]);
             });
         }
+        if constexpr (SC) {
+            const bool bad = emin < kExpLo || emax > kExpHi;
+            if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+                // the exact walk rewrites this block; its stores land after
+                // the scaled walk's (same wave, drained first)
+                __builtin_amdgcn_s_waitcnt(0x0F70);
+                return false;
+            }
+        }
+        return true;
+    }
+
+    // scaled walk first (SMI_SWEEPK_SCALED, default on), the exact walk for
+    // blocks whose inputs leave its range
+    template <int ROW, int CE>
+    __device__ __forceinline__ void go() {
+        if constexpr (kScaled && ROW != ROW_FULL) {
+            if (run<ROW, CE, true>()) return;
+        }
+        run<ROW, CE, false>();
     }
 };
 
@@ -291,19 +376,19 @@ __global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, 
         row = ROW_FULL;
     w.r_begin = row == ROW_BOT ? w.o1 - 1 + K : w.o0 - K;
     switch (row * 4 + ce) {
-    case 0: w.template run<ROW_NONE, 0>(); break;
-    case 1: w.template run<ROW_NONE, 1>(); break;
-    case 2: w.template run<ROW_NONE, 2>(); break;
-    case 3: w.template run<ROW_NONE, 3>(); break;
-    case 4: w.template run<ROW_TOP, 0>(); break;
-    case 5: w.template run<ROW_TOP, 1>(); break;
-    case 6: w.template run<ROW_TOP, 2>(); break;
-    case 7: w.template run<ROW_TOP, 3>(); break;
-    case 8: w.template run<ROW_BOT, 0>(); break;
-    case 9: w.template run<ROW_BOT, 1>(); break;
-    case 10: w.template run<ROW_BOT, 2>(); break;
-    case 11: w.template run<ROW_BOT, 3>(); break;
-    default: w.template run<ROW_FULL, 3>(); break;
+    case 0: w.template go<ROW_NONE, 0>(); break;
+    case 1: w.template go<ROW_NONE, 1>(); break;
+    case 2: w.template go<ROW_NONE, 2>(); break;
+    case 3: w.template go<ROW_NONE, 3>(); break;
+    case 4: w.template go<ROW_TOP, 0>(); break;
+    case 5: w.template go<ROW_TOP, 1>(); break;
+    case 6: w.template go<ROW_TOP, 2>(); break;
+    case 7: w.template go<ROW_TOP, 3>(); break;
+    case 8: w.template go<ROW_BOT, 0>(); break;
+    case 9: w.template go<ROW_BOT, 1>(); break;
+    case 10: w.template go<ROW_BOT, 2>(); break;
+    case 11: w.template go<ROW_BOT, 3>(); break;
+    default: w.template go<ROW_FULL, 3>(); break;
     }
 }
 
