@@ -327,6 +327,52 @@ def aux_gesummv(comm, world: int, rank: int, stream, barrier) -> dict:
             "hbm_frac": round(gbs / (HBM_PEAK_GBS * world), 4)}
 
 
+def aux_kernels_1gpu() -> dict:
+    """N = 1 only: the per-GPU kernels of the 8-GPU configs on one GPU --
+    the config-5 row shard (4096 x 32768 A and B through gemv_rows) and the
+    smi_reduce owner fold of config 4 (8 contributions of 8 Mi fp32 in
+    staging rows 4 KiB apart, as smi_reduce lays them out).  HIP events on
+    the launch stream (include/smi/profiling.h)."""
+    import torch
+    from smi_amd import collectives, gesummv, profiling
+
+    def timed(fn, kern, reps=20):
+        fn()
+        torch.cuda.synchronize()
+        profiling.reset()
+        profiling.enable(True)
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        profiling.enable(False)
+        ms, n = profiling.read(kern)
+        return ms / max(n, 1)
+
+    out = {}
+    n, m = GESUMMV_N // 8, GESUMMV_N
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.rand((n, m), generator=gen, device="cuda")
+    B = torch.rand((n, m), generator=gen, device="cuda")
+    x = torch.rand(m, generator=gen, device="cuda")
+    y = torch.empty(n, device="cuda")
+    ms = timed(lambda: gesummv.gemv_rows(A, B, x, 1.5, 0.5, y), profiling.GEMV)
+    byts = 4 * (2 * n * m + m + n)
+    out["gemv_shard8"] = {"kernel": "gemv_split_kernel (smi_amd/csrc/gesummv.hip)", "rows": n, "cols": m,
+                          "avg_ms": round(ms, 4), "GBs": round(byts / ms / 1e6, 1),
+                          "hbm_frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4)}
+    del A, B
+    cnt, nr, pad = 1 << 23, 8, 1024
+    c = torch.rand((nr, cnt + pad), generator=gen, device="cuda")[:, :cnt]
+    o = torch.empty(cnt, device="cuda")
+    ms = timed(lambda: collectives.reduce_fold(c, "add", o), profiling.REDUCE_FOLD)
+    byts = 4 * cnt * (nr + 1)
+    out["reduce_fold8"] = {"kernel": "fold_kernel<float,4,ADD> (smi_amd/csrc/collectives.hip)",
+                           "contributions": nr, "count": cnt, "row_stride_bytes": 4 * (cnt + pad),
+                           "avg_ms": round(ms, 4), "GBs": round(byts / ms / 1e6, 1),
+                           "hbm_frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4)}
+    return out
+
+
 def aux_p2p(comm, world: int, rank: int, stream, barrier) -> dict:
     """p2p microbenchmarks (microbenchmarks/kernels/bandwidth_*.cl,
     latency_*.cl) over one xGMI link, rank 0 -> rank 1 through smi_send /
@@ -639,8 +685,10 @@ def main() -> None:
             if world > 1:
                 aux["collectives"] = aux_collectives(comm, world, rank, stream, barrier)
                 aux["p2p"] = aux_p2p(comm, world, rank, stream, barrier)
-            elif rank == 0 and not args.no_cpu_baseline:
-                aux["cpu"] = cpu_aux_legs()
+            else:
+                aux["kernels"] = aux_kernels_1gpu()
+                if not args.no_cpu_baseline:
+                    aux["cpu"] = cpu_aux_legs()
         except Exception as e:  # report, never lose the stencil line
             aux["error"] = f"{type(e).__name__}: {e}"
         out["aux"] = aux

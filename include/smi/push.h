@@ -20,8 +20,9 @@ extern "C" {
 
 SMI_Channel SMI_Open_send_channel(int count, SMI_Datatype data_type, int destination, int port,
                                   SMI_Comm comm);
-/* asynch_degree (elements) is accepted for source compatibility; buffering is
- * fixed by the runtime's packet ring. */
+/* asynch_degree (elements; the reference's channel FIFO depth,
+ * codegen/rewrite.py:26-35): at most this many elements are packed before a
+ * message leaves (capped at one 2032-byte payload); <= 0 = the default. */
 SMI_Channel SMI_Open_send_channel_ad(int count, SMI_Datatype data_type, int destination, int port,
                                      SMI_Comm comm, int asynch_degree);
 void SMI_Push_flush(SMI_Channel *chan, void *data, int immediate);

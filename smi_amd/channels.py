@@ -122,17 +122,30 @@ class Channel:
         return self._tmp.value
 
 
-def open_send_channel(count: int, dtype: int, destination: int, port: int, comm: Comm) -> Channel:
-    return Channel(_fn("SMI_Open_send_channel")(count, dtype, destination, port, comm.handle), dtype)
+def open_send_channel(count: int, dtype: int, destination: int, port: int, comm: Comm,
+                      asynch_degree: int | None = None) -> Channel:
+    """SMI_Open_send_channel, or SMI_Open_send_channel_ad when asynch_degree
+    is given (at most that many elements packed per message)."""
+    if asynch_degree is None:
+        return Channel(_fn("SMI_Open_send_channel")(count, dtype, destination, port, comm.handle), dtype)
+    return Channel(_fn("SMI_Open_send_channel_ad")(count, dtype, destination, port, comm.handle, asynch_degree),
+                   dtype)
 
 
-def open_receive_channel(count: int, dtype: int, source: int, port: int, comm: Comm) -> Channel:
-    return Channel(_fn("SMI_Open_receive_channel")(count, dtype, source, port, comm.handle), dtype)
+def open_receive_channel(count: int, dtype: int, source: int, port: int, comm: Comm,
+                         asynch_degree: int | None = None) -> Channel:
+    if asynch_degree is None:
+        return Channel(_fn("SMI_Open_receive_channel")(count, dtype, source, port, comm.handle), dtype)
+    return Channel(_fn("SMI_Open_receive_channel_ad")(count, dtype, source, port, comm.handle, asynch_degree),
+                   dtype)
 
 
 class BChannel:
-    def __init__(self, count, dtype, port, root, comm: Comm):
-        self.c = _fn("SMI_Open_bcast_channel")(count, dtype, port, root, comm.handle)
+    def __init__(self, count, dtype, port, root, comm: Comm, asynch_degree: int | None = None):
+        if asynch_degree is None:
+            self.c = _fn("SMI_Open_bcast_channel")(count, dtype, port, root, comm.handle)
+        else:
+            self.c = _fn("SMI_Open_bcast_channel_ad")(count, dtype, port, root, comm.handle, asynch_degree)
         self._tmp = _Elem(dtype)
         _check(self.c, "SMI_Open_bcast_channel")
 
@@ -144,8 +157,11 @@ class BChannel:
 
 
 class RChannel:
-    def __init__(self, count, dtype, op, port, root, comm: Comm):
-        self.c = _fn("SMI_Open_reduce_channel")(count, dtype, op, port, root, comm.handle)
+    def __init__(self, count, dtype, op, port, root, comm: Comm, asynch_degree: int | None = None):
+        if asynch_degree is None:
+            self.c = _fn("SMI_Open_reduce_channel")(count, dtype, op, port, root, comm.handle)
+        else:
+            self.c = _fn("SMI_Open_reduce_channel_ad")(count, dtype, op, port, root, comm.handle, asynch_degree)
         self._s = _Elem(dtype)
         self._r = _Elem(dtype)
         _check(self.c, "SMI_Open_reduce_channel")

@@ -15,6 +15,7 @@
 // staging slots -- the counterpart of the reference's credit window -- so a
 // rank may push before its peer pops.  Element reduce folds each element's
 // contributions with the same HIP fold kernel as smi_reduce.
+#include <algorithm>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -255,6 +256,25 @@ int take(ChanState *s, int src, void *data) {
     return SMI_SUCCESS;
 }
 
+// asynch_degree (the `_ad` open variants): the reference sizes the channel's
+// FIFO in elements with it (codegen/rewrite.py:26-35), i.e. how far a pusher
+// runs ahead of the wire.  Here it bounds the elements a sender packs before
+// the message leaves (at most one payload); receivers unpack whatever message
+// sizes arrive, so the two ends need not agree and the data never changes.
+template <typename D>
+D with_asynch_degree(D d, int asynch_degree) {
+    if (d.handle && asynch_degree > 0) {
+        ChanState *s = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(g_chan_mu);
+            auto it = g_chans.find(d.handle);
+            if (it != g_chans.end()) s = it->second.get();
+        }
+        if (s) s->per_msg = std::min(s->per_msg, asynch_degree);
+    }
+    return d;
+}
+
 template <typename D>
 ChanState *begin_call(D *chan) {
     if (!chan) return nullptr;
@@ -300,16 +320,14 @@ SMI_Channel SMI_Open_send_channel(int count, SMI_Datatype data_type, int destina
 }
 SMI_Channel SMI_Open_send_channel_ad(int count, SMI_Datatype data_type, int destination, int port, SMI_Comm comm,
                                      int asynch_degree) {
-    (void)asynch_degree;
-    return SMI_Open_send_channel(count, data_type, destination, port, comm);
+    return with_asynch_degree(SMI_Open_send_channel(count, data_type, destination, port, comm), asynch_degree);
 }
 SMI_Channel SMI_Open_receive_channel(int count, SMI_Datatype data_type, int source, int port, SMI_Comm comm) {
     return open_desc<SMI_Channel>(K_P2P, count, data_type, source, port, comm, 0, count);
 }
 SMI_Channel SMI_Open_receive_channel_ad(int count, SMI_Datatype data_type, int source, int port, SMI_Comm comm,
                                         int asynch_degree) {
-    (void)asynch_degree;
-    return SMI_Open_receive_channel(count, data_type, source, port, comm);
+    return with_asynch_degree(SMI_Open_receive_channel(count, data_type, source, port, comm), asynch_degree);
 }
 
 void SMI_Push_flush(SMI_Channel *chan, void *data, int immediate) {
@@ -350,8 +368,7 @@ SMI_BChannel SMI_Open_bcast_channel(int count, SMI_Datatype data_type, int port,
 }
 SMI_BChannel SMI_Open_bcast_channel_ad(int count, SMI_Datatype data_type, int port, int root, SMI_Comm comm,
                                        int asynch_degree) {
-    (void)asynch_degree;
-    return SMI_Open_bcast_channel(count, data_type, port, root, comm);
+    return with_asynch_degree(SMI_Open_bcast_channel(count, data_type, port, root, comm), asynch_degree);
 }
 
 void SMI_Bcast(SMI_BChannel *chan, void *data) {
@@ -389,8 +406,7 @@ SMI_RChannel SMI_Open_reduce_channel(int count, SMI_Datatype data_type, SMI_Op o
 }
 SMI_RChannel SMI_Open_reduce_channel_ad(int count, SMI_Datatype data_type, SMI_Op op, int port, int root,
                                         SMI_Comm comm, int asynch_degree) {
-    (void)asynch_degree;
-    return SMI_Open_reduce_channel(count, data_type, op, port, root, comm);
+    return with_asynch_degree(SMI_Open_reduce_channel(count, data_type, op, port, root, comm), asynch_degree);
 }
 
 void SMI_Reduce(SMI_RChannel *chan, void *data_snd, void *data_rcv) {
@@ -445,8 +461,8 @@ SMI_ScatterChannel SMI_Open_scatter_channel(int send_count, int recv_count, SMI_
 }
 SMI_ScatterChannel SMI_Open_scatter_channel_ad(int send_count, int recv_count, SMI_Datatype data_type, int port,
                                                int root, SMI_Comm comm, int asynch_degree) {
-    (void)asynch_degree;
-    return SMI_Open_scatter_channel(send_count, recv_count, data_type, port, root, comm);
+    return with_asynch_degree(SMI_Open_scatter_channel(send_count, recv_count, data_type, port, root, comm),
+                              asynch_degree);
 }
 
 void SMI_Scatter(SMI_ScatterChannel *chan, void *data_snd, void *data_rcv) {
@@ -486,8 +502,8 @@ SMI_GatherChannel SMI_Open_gather_channel(int send_count, int recv_count, SMI_Da
 }
 SMI_GatherChannel SMI_Open_gather_channel_ad(int send_count, int recv_count, SMI_Datatype data_type, int port,
                                              int root, SMI_Comm comm, int asynch_degree) {
-    (void)asynch_degree;
-    return SMI_Open_gather_channel(send_count, recv_count, data_type, port, root, comm);
+    return with_asynch_degree(SMI_Open_gather_channel(send_count, recv_count, data_type, port, root, comm),
+                              asynch_degree);
 }
 
 void SMI_Gather(SMI_GatherChannel *chan, void *send_data, void *rcv_data) {

@@ -90,6 +90,34 @@ def test_push_before_pop_both_directions(gpu):
     assert all(group(2, fn))
 
 
+@pytest.mark.parametrize("ad", [1, 3, 64, 1 << 20])
+def test_asynch_degree_channels(gpu, ad):
+    """The `_ad` opens (asynch degree = elements packed per message, the
+    reference's FIFO depth): same data for every degree, sender and receiver
+    degrees need not match; p2p, bcast and reduce."""
+    from smi_amd import channels as ch
+
+    def fn(comm):
+        ok = True
+        if comm.rank == 0:
+            c = ch.open_send_channel(777, INT, 1, 0, comm, asynch_degree=ad)
+            for i in range(777):
+                c.push(3 * i)
+        elif comm.rank == 1:
+            c = ch.open_receive_channel(777, INT, 0, 0, comm, asynch_degree=5)
+            ok &= all(c.pop() == 3 * i for i in range(777))
+        b = ch.BChannel(300, FLOAT, 1, 2, comm, asynch_degree=ad)
+        ok &= all(b.bcast(np.float32(i) if comm.rank == 2 else 0) == np.float32(i) for i in range(300))
+        r = ch.RChannel(200, INT, 0, 2, 1, comm, asynch_degree=ad)
+        for i in range(200):
+            v = r.reduce(comm.rank + i)
+            if comm.rank == 1:
+                ok &= v == sum(k + i for k in range(comm.size))
+        return ok
+
+    assert all(group(3, fn))
+
+
 def test_transient_channel_ends_after_count(gpu):
     from smi_amd import SMIError
     from smi_amd import channels as ch

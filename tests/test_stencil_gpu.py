@@ -403,3 +403,43 @@ def test_special_values_bit_exact(gpu, oracle_mod, k, pxpy):
 def test_special_values_single_steps(gpu, oracle_mod):
     g = _special_grid(70, 132, seed=3)
     assert _same(run_steps(g, 5), oracle_mod.stencil(g, 5))
+
+
+# ------------------------------------- the K-step sweep's scaled-level guard --
+def _guard_grid(X, Y, seed):
+    """Uniform [0,1) grid with (a) cells at the edges of the scaled walk's
+    range -- +-2^-100 and the largest float below 2^101, which it accepts --
+    including a patch of +-2^-100(1 + j 2^-23) whose cancellations drive the
+    levels down to multiples of 2^-147, and (b) a few isolated cells outside
+    it (below 2^-100, subnormal, above 2^101), so that only the waves whose
+    cones hold them walk their blocks again with the exact arithmetic."""
+    rng = np.random.default_rng(seed)
+    g = rng.random((X, Y), dtype=np.float32)
+    lo = np.float32(2.0 ** -100)
+    hi = np.nextafter(np.float32(2.0 ** 101), np.float32(0))
+    r0, c0 = X // 5, Y // 6
+    j = np.arange(64 * 48, dtype=np.float32).reshape(64, 48)
+    sgn = np.where((j.astype(np.int64) % 2) == 0, 1, -1).astype(np.float32)
+    g[r0:r0 + 64, c0:c0 + 48] = sgn * lo * (np.float32(1) + (j % 5) * np.float32(2.0 ** -23))
+    g[X // 2, Y // 2] = hi
+    g[X // 2 + 3, Y // 2 - 7] = -hi
+    g[3 * X // 4, Y // 3] = lo
+    for (r, c), v in zip([(X // 8, 7 * Y // 8), (7 * X // 8, Y // 8), (X - 20, Y - 300), (40, Y // 2)],
+                         [1e-35, 1e-40, 3e30, -np.float32(2.0 ** 101)]):
+        g[r, c] = v
+    return g
+
+
+@pytest.mark.parametrize("pxpy", [(1, 1), (2, 2)])
+def test_scaled_guard_mixed_blocks(gpu, oracle_mod, pxpy):
+    PX, PY = pxpy
+    g = _guard_grid(1536, 2048, seed=11 + PX)
+    for T in (12, 27):
+        got = _run_fused(g, T, PX, PY, k=12)
+        assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (pxpy, T)
+
+
+@pytest.mark.parametrize("k", [3, 7, 12])
+def test_scaled_guard_every_k(gpu, oracle_mod, k):
+    g = _guard_grid(700, 1028, seed=k)
+    assert np.array_equal(bits(_run_fused(g, 2 * k + 1, k=k)), bits(oracle_mod.stencil(g, 2 * k + 1)))
