@@ -12,8 +12,8 @@ RCCL over xGMI, overlapped with the interior sweep.  Inputs are resident in
 HBM before the timed region; the timed region is exactly K steps bracketed by
 a barrier + device synchronize on both sides; the time is the max over ranks.
 
-A run of T steps is planned as T // 12 passes of the 12-step sweep plus one
-pass of the remainder (e.g. 20 = 12 + 8; config.plan).  Before the timed
+A run of T steps is planned as ceil(T / 12) sweep passes of at most 12 steps,
+balanced to within one step when T % 12 >= 3 (e.g. 20 = 10 + 10; config.plan).  Before the timed
 region every kernel of that plan launches once and untimed K-step passes run
 for at least --warmup-ms (GPU clock settling).
 

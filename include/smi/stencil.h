@@ -72,8 +72,9 @@ int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
  * Multi-rank runs then exchange depth-K halos -- K rows/columns per side
  * neighbour and a K x K corner block per diagonal neighbour -- once per K
  * steps; a ring kernel computes the K-wide halo-facing band while the
- * interior sweep runs.  Default K = 12.  A run is planned as K-step passes,
- * then ONE pass of the remainder r = timesteps % K when r >= 3, else a pair
+ * interior sweep runs.  Default K = 12.  A run is planned as K-step passes;
+ * a remainder r = timesteps % K >= 3 is spread over ceil(timesteps / K)
+ * passes balanced to within one step (20 = 10 + 10), r = 1 or 2 adds a pair
  * and/or a single step (smi_stencil_plan).  In a multi-rank run K is
  * clipped to half the smaller tile side; tiles smaller than 4 x 8 run single
  * steps only.

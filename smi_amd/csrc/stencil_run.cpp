@@ -187,8 +187,13 @@ static Neighbours neighbours_of(int rank, int px, int py) {
 }
 
 // The phases of a run: K-step passes of the configured K (clipped to what the
-// tile holds: a multi-rank tile needs 2K x 2K), then ONE pass of the
-// remainder when it is 3 or more steps, else a pair and/or a single step.
+// tile holds: a multi-rank tile needs 2K x 2K).  A remainder of 3 or more
+// steps is spread over the passes instead -- the same number of passes,
+// balanced to within one step (T = 20 at K = 12: 10 + 10, not 12 + 8; a pass
+// costs about one HBM sweep whatever its depth, and the deeper one of an
+// unbalanced split pays for its extra levels: 8192^2 T = 20 0.2308 -> 0.2245
+// ms, T = 30 0.3247 -> 0.3178 ms, profiles/r02/plan_split.jsonl); a remainder
+// of 1 or 2 steps stays a pair and/or a single step (12 + 1 beats 7 + 6).
 // Every phase starts from halos of the current state, so the split changes
 // scheduling only, never a bit of the result.
 struct Plan {
@@ -218,11 +223,14 @@ static Plan make_plan(int rows, int cols, int timesteps, bool multi) {
     if (cols < 8 || K < SWEEPK_MIN) K = 0;
     int rest = timesteps;
     if (K) {
-        add(K, rest / K);
-        rest %= K;
-        if (rest >= SWEEPK_MIN) {
-            add(rest, 1);
+        const int passes = rest / K + 1, base = rest / passes, extra = rest % passes;
+        if (rest % K >= SWEEPK_MIN && base >= SWEEPK_MIN) {
+            add(base + 1, extra);
+            add(base, passes - extra);
             rest = 0;
+        } else {
+            add(K, rest / K);
+            rest %= K;
         }
     }
     if (fuse >= 2 && rows >= 4 && cols >= 8) {

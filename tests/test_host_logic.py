@@ -75,18 +75,25 @@ def test_bench_halo_report_counts_neighbours():
 
 
 # ------------------------------------------------------------ run planner --
-def test_plan_splits_steps_into_deep_passes_and_one_remainder():
-    """smi_stencil_plan (host only): T // 12 passes of 12 steps, then ONE pass
-    of the remainder r when r >= 3, else a pair and/or a single step."""
+def test_plan_splits_steps_into_balanced_deep_passes():
+    """smi_stencil_plan (host only): a remainder r = T % 12 >= 3 is spread
+    over ceil(T / 12) passes balanced to within one step; r = 1 or 2 stays
+    T // 12 passes of 12 and a pair or a single step."""
     from smi_amd import stencil
     for T in range(0, 60):
         ph = stencil.plan(8192, 8192, 1, 1, 0, T)["phases"]
         assert sum(k * n for k, n in ph) == T
         q, r = divmod(T, 12)
-        want = ([(12, q)] if q else []) + ([(r, 1)] if r >= 3 else ([(r, 1)] if r else []))
+        if r >= 3:
+            base, extra = divmod(T, q + 1)
+            want = ([(base + 1, extra)] if extra else []) + [(base, q + 1 - extra)]
+        else:
+            want = ([(12, q)] if q else []) + ([(r, 1)] if r else [])
         assert ph == want, (T, ph)
+        assert max(k for k, _ in ph or [(0, 0)]) - min(k for k, _ in ph or [(0, 0)]) <= (1 if r >= 3 else 12)
         assert stencil.plan(8192, 8192, 1, 1, 0, T)["result_index"] == sum(n for _, n in ph) % 2
-    assert stencil.plan(8192, 8192, 1, 1, 0, 20)["phases"] == [(12, 1), (8, 1)]  # the driver's --steps 20
+    assert stencil.plan(8192, 8192, 1, 1, 0, 20)["phases"] == [(10, 2)]  # the driver's --steps 20
+    assert stencil.plan(8192, 8192, 1, 1, 0, 2400)["phases"] == [(12, 200)]  # bench defaults
 
 
 def test_plan_neighbours_follow_reference_rank_map():
@@ -104,7 +111,7 @@ def test_plan_neighbours_follow_reference_rank_map():
 
 def test_plan_clips_k_to_the_tile():
     from smi_amd import stencil
-    assert stencil.plan(10, 16, 2, 2, 0, 23)["phases"] == [(5, 4), (3, 1)]
+    assert stencil.plan(10, 16, 2, 2, 0, 23)["phases"] == [(5, 3), (4, 2)]   # K clipped to 5, balanced
     assert stencil.plan(10, 16, 1, 1, 0, 23)["phases"] == [(12, 1), (11, 1)]  # single tile: no halo limit
     assert stencil.plan(4, 4, 1, 1, 0, 5)["phases"] == [(1, 5)]                # below 4 x 8: single steps
     assert stencil.plan(4, 8, 2, 2, 0, 5)["phases"] == [(2, 2), (1, 1)]
@@ -125,7 +132,7 @@ def test_fusion_setting_drives_the_plan():
     old = stencil.get_fusion()
     try:
         stencil.set_fusion(8)
-        assert stencil.plan(256, 256, 1, 1, 0, 20)["phases"] == [(8, 2), (4, 1)]
+        assert stencil.plan(256, 256, 1, 1, 0, 20)["phases"] == [(7, 2), (6, 1)]
         stencil.set_fusion(2)
         assert stencil.plan(256, 256, 1, 1, 0, 7)["phases"] == [(2, 3), (1, 1)]
         stencil.set_fusion(1)

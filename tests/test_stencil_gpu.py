@@ -285,7 +285,7 @@ def test_deep_full_size_8192(gpu, oracle_mod):
 
 def test_bench_config_full_size_k12(gpu, oracle_mod):
     """BASELINE config 2 exactly as bench.py runs it: 8192^2 fp32, the default
-    K = 12 and automatic row blocks, T = 12 (one pass), 20 (12 + 8: the
+    K = 12 and automatic row blocks, T = 12 (one pass), 20 (10 + 10: the
     driver's --steps 20) and 25 (12 + 12 + 1), bit-exact vs the oracle."""
     from smi_amd import LocalGroup, stencil
     assert stencil.get_fusion()["steps_per_pass"] == 12
@@ -331,7 +331,7 @@ def test_clipped_k_on_small_tiles(gpu, oracle_mod):
     """Tiles smaller than 24 x 24 in a multi-rank run clip K to half the
     smaller side (here 10 x 16 tiles: K = 5) instead of dropping to pairs."""
     from smi_amd import stencil
-    assert stencil.plan(10, 16, 2, 2, 0, 23)["phases"] == [(5, 4), (3, 1)]
+    assert stencil.plan(10, 16, 2, 2, 0, 23)["phases"] == [(5, 3), (4, 2)]
     g = oracle_mod.init_uniform(20, 32, seed=5)
     assert np.array_equal(bits(_run_fused(g, 23, 2, 2, k=12)), bits(oracle_mod.stencil(g, 23)))
 
