@@ -201,8 +201,9 @@ def pmc_traffic(cells: int, steps_per_launch: int) -> float | None:
     try:
         with open(PMC_FILE) as f:
             d = json.load(f)
-        if int(d.get("cells", -1)) == cells and int(d.get("steps_per_launch", 1)) == steps_per_launch:
-            return float(d["hbm_bytes_per_launch"])
+        for e in d.get("entries", [d]):
+            if int(e.get("cells", -1)) == cells and int(e.get("steps_per_launch", 1)) == steps_per_launch:
+                return float(e["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError):
         pass
     return None
