@@ -454,6 +454,7 @@ def aux_collectives(comm, world: int, rank: int, stream, barrier) -> list:
             t_rf = _timed_runs(lambda: collectives.reduce(comm, snd_f, rcv, "add", root=root, stream=stream),
                                iters, barrier, world)
             t_b = _timed_runs(lambda: collectives.bcast(comm, buf, root=0, stream=stream), iters, barrier, world)
+        sys.stderr.write(f"[bench rank {rank}] aux collectives {nbytes} B done\n")
         ok = True
         if rank == root:  # KAT: sum of (rank + 1) = n(n+1)/2 (microbenchmarks/kernels/reduce.cl:13-24)
             ok = bool((rcv_i == world * (world + 1) // 2).all().item())
@@ -484,11 +485,24 @@ def main() -> None:
                     help="skip the gesummv / reduce / bcast lines measured after the timed stencil region")
     args = ap.parse_args()
 
+    # stdout carries exactly one line, the result: anything the libraries
+    # underneath write there (RCCL's version banner, gloo's connection notes,
+    # from C as well as Python) goes to stderr instead
+    result_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
     import smi_amd
     from smi_amd import profiling, stencil
+
+    t_start = time.perf_counter()
+
+    def log(what):  # progress on stderr (stdout carries only the result line)
+        sys.stderr.write(f"[bench rank {os.environ.get('RANK', '0')} +{time.perf_counter() - t_start:.1f}s] {what}\n")
+        sys.stderr.flush()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -502,6 +516,7 @@ def main() -> None:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
         comm = smi_amd.Comm.from_env(device=local)
+        log("RCCL communicator up")
     else:
         comm = smi_amd.LocalGroup(1, device=local).comm(0)
 
@@ -523,6 +538,8 @@ def main() -> None:
     with torch.cuda.stream(stream):
         if args.warmup:
             stencil.run(comm, tile, args.warmup, PX, PY, scratch)
+            torch.cuda.synchronize()
+            log(f"{args.warmup} warm-up steps done")
         # HIP loads a kernel's code object at its first launch: every kernel
         # of the timed plan (the K-step passes and the remainder pass) runs
         # once outside the timed region ...
@@ -532,6 +549,7 @@ def main() -> None:
         for k, _ in plan["phases"]:
             stencil.run(comm, tile, k, PX, PY, scratch)
         torch.cuda.synchronize()
+        log("every kernel of the plan launched once")
         profiling.enable(False)
         profiling.reset()
         # ... and the GPU clock needs tens of ms of load to settle (120 steps
@@ -543,6 +561,7 @@ def main() -> None:
             stencil.run(comm, tile, max(K, 1) * 4, PX, PY, scratch)
             torch.cuda.synchronize()
         warm_ms = (time.perf_counter() - t_w) * 1e3
+        log(f"warm-up floor done ({warm_ms:.1f} ms)")
         barrier()
         torch.cuda.synchronize()
         profiling.reset()
@@ -554,6 +573,7 @@ def main() -> None:
         t1 = time.perf_counter()
         profiling.enable(False)
     elapsed = t1 - t0
+    log(f"timed region done: {args.steps} steps in {elapsed * 1e3:.3f} ms")
     # Every stencil kernel launched in the timed region, with its measured
     # time (HIP events around each launch on its own stream); the roofline
     # prices the one that took the most time.
@@ -668,7 +688,9 @@ def main() -> None:
 
     def emit(o):
         if rank == 0 and printed.acquire(blocking=False):
-            print(json.dumps(o), flush=True)
+            data = (json.dumps(o) + "\n").encode()
+            while data:
+                data = data[os.write(result_fd, data):]
 
     def watchdog():
         o = dict(out)
@@ -683,9 +705,12 @@ def main() -> None:
         aux = {}
         try:
             aux["gesummv"] = aux_gesummv(comm, world, rank, stream, barrier)
+            log("aux gesummv done")
             if world > 1:
                 aux["collectives"] = aux_collectives(comm, world, rank, stream, barrier)
+                log("aux collectives done")
                 aux["p2p"] = aux_p2p(comm, world, rank, stream, barrier)
+                log("aux p2p done")
             else:
                 aux["kernels"] = aux_kernels_1gpu()
                 if not args.no_cpu_baseline:
