@@ -156,6 +156,7 @@ struct RingKArgs {
     // filled by launch_ringk: band rectangles and block prefix
     int r0[4], r1[4], c0[4], c1[4];
     int first_block[5];
+    int exp_mode;      // timing experiments (rehearsal build, SMI_RING_EXP): 1 no levels, 2 no loads, 4 no stores
 };
 int launch_ringk(RingKArgs a, hipStream_t s);
 int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s);

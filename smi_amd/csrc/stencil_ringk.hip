@@ -12,42 +12,56 @@
 // corner blocks for the next exchange.  The per-cell arithmetic and the
 // global-edge copy rule are the sweep's (stencil_smi.cl:143-156); cells of
 // the apron that lie outside the global grid are never used by a stored cell.
+#include <cstdlib>
+
 #include "stencil_common.h"
 
 namespace smi {
 
-// extended-tile cell (p, q), p in [-K, X+K), q in [-K, Y+K); 0 where no data
-// exists (outside the global grid: only ever read by unused cells)
-__device__ __forceinline__ float ext_at(const RingKArgs &a, int p, int q) {
+// extended-tile cell (p, q), p in [-K, X+K), q in [-K, Y+K): the address it
+// is read from, or nullptr where no data exists (outside the global grid:
+// only ever read by unused cells).  Branch-free (selects only), so a thread's
+// loads of all its cells issue back to back.
+__device__ __forceinline__ const float *ext_ptr(const RingKArgs &a, int p, int q) {
     const int X = a.rows, Y = a.cols, K = a.k;
     const bool pin = p >= 0 && p < X, qin = q >= 0 && q < Y;
-    // every index is clamped into its buffer, so a load the compiler
-    // executes ahead of its branch can never leave the allocation
     const int pc = min(max(p, 0), X - 1), qc = min(max(q, 0), Y - 1);
-    if (pin && qin) return a.in[(size_t)pc * Y + qc];
-    if (qin) {
-        if (p < 0) return a.has[0] ? a.h.top[(size_t)max(p + K, 0) * Y + qc] : 0.f;
-        return a.has[1] ? a.h.bot[(size_t)min(p - X, K - 1) * Y + qc] : 0.f;
-    }
-    if (pin) {
-        if (q < 0) return a.has[2] ? a.h.left[(size_t)pc * K + max(q + K, 0)] : 0.f;
-        return a.has[3] ? a.h.right[(size_t)pc * K + min(q - Y, K - 1)] : 0.f;
-    }
+    const int hr = p < 0 ? max(p + K, 0) : min(p - X, K - 1);  // halo row (top / bottom)
+    const int hc = q < 0 ? max(q + K, 0) : min(q - Y, K - 1);  // halo column (left / right)
+    const float *tile = a.in + (size_t)pc * Y + qc;
+    const float *vert = (p < 0 ? a.h.top : a.h.bot) + (size_t)hr * Y + qc;
+    const float *horz = (q < 0 ? a.h.left : a.h.right) + (size_t)pc * K + hc;
     const int ci = (p < 0 ? 0 : 2) + (q < 0 ? 0 : 1);  // tl, tr, bl, br
-    if (!a.has_diag[ci]) return 0.f;
-    const int i = min(max(p < 0 ? p + K : p - X, 0), K - 1);
-    const int j = min(max(q < 0 ? q + K : q - Y, 0), K - 1);
-    return a.h.corner[ci][i * K + j];
+    const float *corn = a.h.corner[ci] + hr * K + hc;
+    const bool has_v = p < 0 ? a.has[0] : a.has[1];
+    const bool has_h = q < 0 ? a.has[2] : a.has[3];
+    const float *src = (pin && qin) ? tile : qin ? (has_v ? vert : nullptr)
+                       : pin ? (has_h ? horz : nullptr) : (a.has_diag[ci] ? corn : nullptr);
+    return src;
 }
 
 // Output blocks: top/bottom bands in K x RB_W blocks, left/right bands in
 // RB_H x K blocks (block b -> band via the prefix table in RingKArgs).  K is
 // a runtime value (the depth of the current phase); LDS is sized for
 // RING_KMAX.
+//
+// The block's H x W region (output block + K apron) is dealt to the threads
+// once: thread t owns cells t, t + 256, ... (at most RING_CELLS) and keeps
+// each cell's depth (distance to the region's edge: the cell is valid at
+// levels 1..depth; 0 for a global-edge cell, which is copied) in a register,
+// so the K level sweeps are divide- and branch-free.  (Round 1 recomputed the coordinates with a division per cell per
+// level: 35 us per pass at 8192^2, K = 12, which an interior rank could not
+// hide behind its 0.11 ms interior sweep -- tools/rehearsal.py measured 0.78
+// of a lone tile's rate.)
+constexpr int RING_CELLS = (3 * RING_KMAX * ((RB_W > RB_H ? RB_W : RB_H) + 2 * RING_KMAX) + 255) / 256;
+
 __global__ __launch_bounds__(256) void ringk_kernel(RingKArgs a) {
-    // horizontal blocks: 3K x (RB_W + 2K); vertical blocks: (RB_H + 2K) x 3K
+    // horizontal blocks: 3K x (RB_W + 2K); vertical blocks: (RB_H + 2K) x 3K;
+    // PAD floats before and after each buffer keep the neighbour reads of the
+    // region's border cells inside the allocation (their results are unused)
     constexpr int LDS_N = 3 * RING_KMAX * ((RB_W > RB_H ? RB_W : RB_H) + 2 * RING_KMAX);
-    __shared__ float lds[2][LDS_N];
+    constexpr int PAD = (RB_W > RB_H ? RB_W : RB_H) + 2 * RING_KMAX + 4;
+    __shared__ float lds[2][LDS_N + 2 * PAD];
     const int K = a.k;
     const int b = blockIdx.x;
     int band = 0;
@@ -63,32 +77,56 @@ __global__ __launch_bounds__(256) void ringk_kernel(RingKArgs a) {
     const int pb = oR0 - K, qb = oC0 - K;  // extended coordinates of lds (0,0)
     const int X = a.rows, Y = a.cols;
     const bool gT = !a.has[0], gB = !a.has[1], gL = !a.has[2], gR = !a.has[3];
+    const int n = H * W;
+    float *L0 = lds[0] + PAD, *L1 = lds[1] + PAD;
 
-    for (int i = threadIdx.x; i < H * W; i += 256) {
-        const int y = i / W, x = i - y * W;
-        lds[0][i] = ext_at(a, pb + y, qb + x);
+    int dep[RING_CELLS];   // levels the cell is computed at (1..dep); 0 for a copied cell
+#pragma unroll
+    for (int j = 0; j < RING_CELLS; ++j) {
+        const int i = threadIdx.x + 256 * j;
+        dep[j] = 0;
+        if (i < n) {
+            const int y = i / W, x = i - y * W;
+            const int p = pb + y, q = qb + x;
+            const bool copy = (p == 0 && gT) || (p == X - 1 && gB) || (q == 0 && gL) || (q == Y - 1 && gR);
+            dep[j] = copy ? 0 : min(min(y, H - 1 - y), min(x, W - 1 - x));
+            const float *src = (a.exp_mode & 2) ? nullptr : ext_ptr(a, p, q);
+            const float v = *(src ? src : a.in);  // unconditional load (a.in: any valid address)
+            L0[i] = src ? v : 0.f;
+        }
     }
     __syncthreads();
+    // Branch-free level sweeps: every cell of the region is rewritten each
+    // level -- the new value where it is valid (depth >= l), its old value
+    // elsewhere (copied cells keep theirs; cells shallower than l are never
+    // read by a valid one) -- so all LDS reads of a level issue together.
 #pragma unroll 1
-    for (int l = 1; l <= K; ++l) {
-        const float *src = lds[(l - 1) & 1];
-        float *dst = lds[l & 1];
-        const int hl = H - 2 * l, wl = W - 2 * l;
-        for (int i = threadIdx.x; i < hl * wl; i += 256) {
-            const int y = l + i / wl, x = l + i % wl;
-            const int p = pb + y, q = qb + x;
-            const int o = y * W + x;
-            const bool copy = (p == 0 && gT) || (p == X - 1 && gB) || (q == 0 && gL) || (q == Y - 1 && gR);
-            dst[o] = copy ? src[o] : jacobi(src[o + W], src[o - 1], src[o + 1], src[o - W]);
+    for (int l = 1; l <= ((a.exp_mode & 1) ? 0 : K); ++l) {
+        const float *src = (l & 1) ? L0 : L1;
+        float *dst = (l & 1) ? L1 : L0;
+        float v[RING_CELLS];
+#pragma unroll
+        for (int j = 0; j < RING_CELLS; ++j) {
+            const int o = min(threadIdx.x + 256 * j, n - 1);
+            const float nv = jacobi(src[o + W], src[o - 1], src[o + 1], src[o - W]);
+            v[j] = dep[j] >= l ? nv : src[o];
+        }
+#pragma unroll
+        for (int j = 0; j < RING_CELLS; ++j) {
+            const int o = threadIdx.x + 256 * j;
+            if (o < n) dst[o] = v[j];
         }
         __syncthreads();
     }
-    const float *res = lds[K & 1];
-    const int oh = oR1 - oR0, ow = oC1 - oC0;
-    for (int i = threadIdx.x; i < oh * ow; i += 256) {
-        const int y = i / ow, x = i - y * ow;
-        const int p = oR0 + y, q = oC0 + x;
-        const float v = res[(y + K) * W + (x + K)];
+    const float *res = (K & 1) ? L1 : L0;
+#pragma unroll
+    for (int j = 0; j < RING_CELLS; ++j) {
+        const int o = threadIdx.x + 256 * j;
+        if (o >= n || (a.exp_mode & 4)) continue;
+        const int y = o / W, x = o - y * W;
+        if (y < K || y >= H - K || x < K || x >= W - K) continue;  // apron cell: not an output
+        const int p = pb + y, q = qb + x;
+        const float v = res[o];
         a.out[(size_t)p * Y + q] = v;
         if (!a.pack) continue;
         if (q < K) a.h.send_left[(size_t)p * K + q] = v;
@@ -150,6 +188,10 @@ int launch_ringk(RingKArgs a, hipStream_t s) {
     }
     a.first_block[4] = nb;
     if (nb == 0) return SMI_SUCCESS;
+    a.exp_mode = 0;
+#ifdef SMI_LOOPBACK_REHEARSAL
+    if (const char *e = getenv("SMI_RING_EXP")) a.exp_mode = atoi(e);
+#endif
     int tok = -1;
     if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_EDGE, s, &tok));
     hipLaunchKernelGGL(ringk_kernel, dim3(nb), dim3(256), 0, s, a);
