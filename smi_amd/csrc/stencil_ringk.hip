@@ -53,9 +53,11 @@ __device__ __forceinline__ const float *ext_ptr(const RingKArgs &a, int p, int q
 // level: 35 us per pass at 8192^2, K = 12, which an interior rank could not
 // hide behind its 0.11 ms interior sweep -- tools/rehearsal.py measured 0.78
 // of a lone tile's rate.)
-constexpr int RING_CELLS = (3 * RING_KMAX * ((RB_W > RB_H ? RB_W : RB_H) + 2 * RING_KMAX) + 255) / 256;
+constexpr int RING_REGION = 3 * RING_KMAX * ((RB_W > RB_H ? RB_W : RB_H) + 2 * RING_KMAX);
 
-__global__ __launch_bounds__(256) void ringk_kernel(RingKArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void ringk_kernel(RingKArgs a) {
+    constexpr int RING_CELLS = (RING_REGION + NT - 1) / NT;
     // horizontal blocks: 3K x (RB_W + 2K); vertical blocks: (RB_H + 2K) x 3K;
     // PAD floats before and after each buffer keep the neighbour reads of the
     // region's border cells inside the allocation (their results are unused)
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(256) void ringk_kernel(RingKArgs a) {
     int dep[RING_CELLS];   // levels the cell is computed at (1..dep); 0 for a copied cell
 #pragma unroll
     for (int j = 0; j < RING_CELLS; ++j) {
-        const int i = threadIdx.x + 256 * j;
+        const int i = threadIdx.x + NT * j;
         dep[j] = 0;
         if (i < n) {
             const int y = i / W, x = i - y * W;
@@ -107,13 +109,13 @@ __global__ __launch_bounds__(256) void ringk_kernel(RingKArgs a) {
         float v[RING_CELLS];
 #pragma unroll
         for (int j = 0; j < RING_CELLS; ++j) {
-            const int o = min(threadIdx.x + 256 * j, n - 1);
+            const int o = min((int)threadIdx.x + NT * j, n - 1);
             const float nv = jacobi(src[o + W], src[o - 1], src[o + 1], src[o - W]);
             v[j] = dep[j] >= l ? nv : src[o];
         }
 #pragma unroll
         for (int j = 0; j < RING_CELLS; ++j) {
-            const int o = threadIdx.x + 256 * j;
+            const int o = threadIdx.x + NT * j;
             if (o < n) dst[o] = v[j];
         }
         __syncthreads();
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(256) void ringk_kernel(RingKArgs a) {
     const float *res = (K & 1) ? L1 : L0;
 #pragma unroll
     for (int j = 0; j < RING_CELLS; ++j) {
-        const int o = threadIdx.x + 256 * j;
+        const int o = threadIdx.x + NT * j;
         if (o >= n || (a.exp_mode & 4)) continue;
         const int y = o / W, x = o - y * W;
         if (y < K || y >= H - K || x < K || x >= W - K) continue;  // apron cell: not an output
@@ -194,7 +196,16 @@ int launch_ringk(RingKArgs a, hipStream_t s) {
 #endif
     int tok = -1;
     if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_EDGE, s, &tok));
-    hipLaunchKernelGGL(ringk_kernel, dim3(nb), dim3(256), 0, s, a);
+    int nt = 256;
+#ifdef SMI_LOOPBACK_REHEARSAL
+    if (const char *e = getenv("SMI_RING_THREADS")) nt = atoi(e);
+#endif
+    if (nt == 64)
+        hipLaunchKernelGGL(ringk_kernel<64>, dim3(nb), dim3(64), 0, s, a);
+    else if (nt == 128)
+        hipLaunchKernelGGL(ringk_kernel<128>, dim3(nb), dim3(128), 0, s, a);
+    else
+        hipLaunchKernelGGL(ringk_kernel<256>, dim3(nb), dim3(256), 0, s, a);
     SMI_HIP_CHECK(hipGetLastError());
     if (tok >= 0) SMI_TRY(prof_end(tok, s));
     return SMI_SUCCESS;

@@ -1,5 +1,7 @@
 // stencilk.hip -- host side of the K-step sweep (kernel: stencilk.h, one
 // instantiation per K in stencilk_k<K>.hip).
+#include <cstdlib>
+
 #include "stencil_common.h"
 
 namespace smi {
@@ -51,7 +53,12 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
         // retire during the pass and the high-priority ring kernel and RCCL
         // exchange on the comm stream are dispatched then, instead of waiting
         // for the whole interior pass.
-        const int waves = resident_waves(K);
+        int waves = resident_waves(K);
+#ifdef SMI_LOOPBACK_REHEARSAL
+        // experiment: leave a share of the wave slots to the ring kernel
+        if (const char *e = getenv("SMI_INTERIOR_PCT"))
+            if (!(a.gT && a.gB && a.gL && a.gR)) waves = std::max(1, waves * atoi(e) / 100);
+#endif
         const bool single = a.gT && a.gB && a.gL && a.gR;
         int rounds_multi = g_tune.rounds_multi;
 #ifdef SMI_LOOPBACK_REHEARSAL
