@@ -68,6 +68,13 @@
 #ifndef SMI_SWEEPK_SCALED
 #define SMI_SWEEPK_SCALED 1
 #endif
+// experiment switches (tools/sweepbench builds; the library uses the defaults)
+#ifndef SMI_SWEEPK_NT_LOADS
+#define SMI_SWEEPK_NT_LOADS 0
+#endif
+#ifndef SMI_SWEEPK_TASK_ORDER
+#define SMI_SWEEPK_TASK_ORDER 0
+#endif
 
 namespace smi {
 
@@ -141,7 +148,13 @@ struct SweepK {
     template <bool REV>
     __device__ __forceinline__ float4 ld(int t) const {
         const int r = min(max(REV ? r_begin - t : r_begin + t, 0), rows - 1);
+#if SMI_SWEEPK_NT_LOADS
+        typedef float V4 __attribute__((ext_vector_type(4)));
+        const V4 v = __builtin_nontemporal_load(reinterpret_cast<const V4 *>(in + (size_t)r * cols + cl));
+        return make_float4(v.x, v.y, v.z, v.w);
+#else
         return *reinterpret_cast<const float4 *>(in + (size_t)r * cols + cl);
+#endif
     }
 
     // One level step of 4 cells per lane.  SC (scaled): the operands carry
@@ -340,8 +353,14 @@ __global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, 
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
     const int task = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
+#if SMI_SWEEPK_TASK_ORDER == 1  // experiment: consecutive tasks walk consecutive row blocks of one strip
+    const int strip = task / nrb;
+    const int rb = task - strip * nrb;
+    if (strip >= nstrips) return;
+#else
     const int rb = task / nstrips;
     const int strip = task - rb * nstrips;
+#endif
     if (rb >= nrb) return;  // wave-uniform
 
     S w;
