@@ -125,6 +125,7 @@ constexpr int SWEEPK_MIN = 3, SWEEPK_MAX = 12;
 // stores), else the minimal ceil(K / 4).
 __host__ __device__ constexpr int sweepk_apron_lanes(int K) { return K >= 9 ? 4 : (K + 3) / 4; }
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s);
+int launch_sweepk_ex(int K, const SweepKArgs &a, int ht, int reserve, bool prof, hipStream_t s);
 int sweepk_window_cols(int K);  // output columns per 256-column window
 
 // Depth-K halos (stencil_ringk.hip).  Receive side: top = rows -K..-1 and
@@ -159,6 +160,24 @@ struct RingKArgs {
     int exp_mode;      // timing experiments (rehearsal build, SMI_RING_EXP): 1 no levels, 2 no loads, 4 no stores
 };
 int launch_ringk(RingKArgs a, hipStream_t s);
+
+// The same halo-facing bands as register sweeps (stencil_bands.hip): the
+// extended-tile rows/columns the bands need are gathered into two small
+// images -- H: the top band's rows [-K, 2K) over [Y + aprons] columns stacked
+// on the bottom band's rows [X-2K, X+K); V: the tile's rows with the left
+// band's columns [-KC, 2KC) beside the right band's [Y-2KC, Y+KC) -- swept by
+// sweepk_kernel<K> with few, tall row blocks, and scattered back into the
+// tile with the next exchange's sends.  About 100 waves in all, so they run
+// beside an interior sweep that leaves them their slots.
+struct BandImages {
+    float *h_in, *h_out;  // 6K x wi
+    float *v_in, *v_out;  // rows x 6KC
+};
+size_t band_images_elems(int rows, int cols, int K);
+bool bands_eligible(int rows, int cols, int K);
+BandImages band_images_at(float *base, int rows, int cols, int K);
+constexpr int BAND_RESERVE_WAVES = 160;  // interior waves left to the band sweeps + exchange
+int launch_ring_bands(const RingKArgs &a, const BandImages &im, hipStream_t s);
 int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s);
 #ifdef SMI_LOOPBACK_REHEARSAL
 int launch_multicopy(const float *const *src, float *const *dst, const size_t *bytes, int nseg, hipStream_t s);

@@ -415,7 +415,18 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     const size_t need2 = 4 * (size_t)cols + 8 * (size_t)rows + 8;
     const size_t needk =
         kmax ? 2 * (size_t)kmax * cols + 4 * (size_t)rows * kmax + 8 * (size_t)kmax * kmax : 0;
-    SMI_TRY(ensure_halo(c, need2 + needk));
+    // Halo-facing bands of the K-step passes: the LDS ring kernel (default),
+    // or -- SMI_RING_MODE=1, an experiment -- register sweeps over gathered
+    // band images (stencil_bands.hip).  Bit-identical either way; the band
+    // sweeps lost on the interior-rank rehearsal (0.50 vs 0.76-0.79 of a lone
+    // tile): their chain of six small kernels is latency-bound under the
+    // interior's saturated HBM (gather 28 -> 74 us, band sweeps 20 + 31 ->
+    // 56 + 66 us when run beside it; profiles/r02/rehearsal/bands_*).
+    const char *rm = getenv("SMI_RING_MODE");
+    const bool bands = kmax && rm && atoi(rm) != 0 && bands_eligible(rows, cols, kmax);
+    const size_t needb = bands ? band_images_elems(rows, cols, kmax) : 0;
+    const size_t offb = (need2 + needk + 3) / 4 * 4;
+    SMI_TRY(ensure_halo(c, offb + needb));
     Halo2Buf hb;
     hb.top2 = c->halo;
     hb.bot2 = hb.top2 + 2 * (size_t)cols;
@@ -516,12 +527,21 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             };
             SMI_TRY(launch_packk(bufp(cur), rows, cols, K, hkv, cs));
             SMI_TRY(xchgk(bufp(cur), cs));
+            const bool use_bands = bands && bands_eligible(rows, cols, K);
+            const BandImages im = use_bands ? band_images_at(c->halo + offb, rows, cols, K) : BandImages{};
             for (int p = 0; p < npass; ++p, cur ^= 1) {
                 rk.in = ak.in = bufp(cur);
                 rk.out = ak.out = bufp(cur ^ 1);
-                SMI_TRY(pass([&](hipStream_t st) { return launch_ringk(rk, st); },
-                             [&](hipStream_t st) { return launch_sweepk(K, ak, st); }, xchgk, p < npass - 1,
-                             ak.out));
+                if (use_bands)
+                    SMI_TRY(pass([&](hipStream_t st) { return launch_ring_bands(rk, im, st); },
+                                 [&](hipStream_t st) {
+                                     return launch_sweepk_ex(K, ak, 0, overlap ? BAND_RESERVE_WAVES : 0, true, st);
+                                 },
+                                 xchgk, p < npass - 1, ak.out));
+                else
+                    SMI_TRY(pass([&](hipStream_t st) { return launch_ringk(rk, st); },
+                                 [&](hipStream_t st) { return launch_sweepk(K, ak, st); }, xchgk, p < npass - 1,
+                                 ak.out));
             }
         } else if (K == 2) {
             // ---- pairs of steps (depth-2 halos)

@@ -37,7 +37,14 @@ static int resident_waves(int K) {
 
 int sweepk_window_cols(int K) { return 256 - 8 * sweepk_apron_lanes(K); }
 
-int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
+int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) { return launch_sweepk_ex(K, a, 0, 0, true, s); }
+
+// ht > 0: rows per wave as given; else automatic (g_tune.htk, or one round
+// of resident waves -- minus `reserve` waves left to the comm stream's
+// kernels in a multi-rank run).  prof: record the launch under
+// SMI_PROF_STENCIL_SWEEPK (the ring's band sweeps are recorded by their
+// caller instead).
+int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool prof, hipStream_t s) {
     if (a.row_hi <= a.row_lo || a.col_hi <= a.col_lo) return SMI_SUCCESS;
     SMI_ARG_CHECK(K >= SWEEPK_MIN && K <= SWEEPK_MAX, "sweepk: steps per pass must be 3..12");
     SMI_ARG_CHECK(a.cols % 4 == 0 && a.col_lo % 4 == 0 && a.col_hi % 4 == 0, "sweepk: columns not float4 aligned");
@@ -46,13 +53,14 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
     const int sw = sweepk_window_cols(K);
     const int nstrips = (a.col_hi - a.col_lo + sw - 1) / sw;
     const int out_rows = a.row_hi - a.row_lo;
-    int ht = g_tune.htk;
+    int ht = ht_req > 0 ? ht_req : g_tune.htk;
     if (ht <= 0) {
         // auto: one round of resident waves, each a tall row block of its
-        // strip.  Multi-rank interior: several rounds, so that workgroups
-        // retire during the pass and the high-priority ring kernel and RCCL
-        // exchange on the comm stream are dispatched then, instead of waiting
-        // for the whole interior pass.
+        // strip.  Multi-rank interior: either leave `reserve` waves to the
+        // ring's band sweeps and the exchange on the comm stream (one round
+        // of the rest), or cut the interior into several rounds so that
+        // workgroups retire during the pass and the comm stream's kernels are
+        // dispatched then.
         int waves = resident_waves(K);
 #ifdef SMI_LOOPBACK_REHEARSAL
         // experiment: leave a share of the wave slots to the ring kernel
@@ -64,7 +72,11 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
 #ifdef SMI_LOOPBACK_REHEARSAL
         if (const char *e = getenv("SMI_ROUNDS_MULTI")) rounds_multi = atoi(e);
 #endif
-        const int rounds = single ? 1 : std::max(1, rounds_multi);
+        int rounds = single ? 1 : std::max(1, rounds_multi);
+        if (!single && reserve > 0) {
+            waves = std::max(64, waves - reserve);
+            rounds = 1;
+        }
         const int per_strip = std::max(1, waves * rounds / nstrips);
         ht = std::max(2 * K, (out_rows + per_strip - 1) / per_strip);
     }
@@ -72,7 +84,7 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) {
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
     int tok = -1;
-    if (prof_enabled())
+    if (prof && prof_enabled())
         SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K));
     int rc = SMI_SUCCESS;
     switch (K) {
