@@ -7,6 +7,8 @@
 #include <mutex>
 #include <unordered_map>
 
+#include <cstdlib>
+
 #include "smi_internal.h"
 
 namespace smi {
@@ -78,7 +80,11 @@ static int finish_init(std::unique_ptr<Comm> c, SMI_Comm *out) {
     // the critical path, the interior sweep beside them is not
     int least = 0, greatest = 0;
     SMI_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    SMI_HIP_CHECK(hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, greatest));
+    int prio = greatest;
+#ifdef SMI_LOOPBACK_REHEARSAL
+    if (getenv("SMI_COMM_LOW_PRIORITY")) prio = least;  // experiment: ring in the interior's tail
+#endif
+    SMI_HIP_CHECK(hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
     return register_comm(std::move(c), out);
 }
 

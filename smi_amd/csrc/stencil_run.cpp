@@ -493,9 +493,18 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             // event + copy per message in-process) that must not delay the
             // interior's launch -- the trace of an interior rank showed the
             // main stream idle ~100 us per pass behind the exchange calls.
-            SMI_TRY(ring(cs));
-            SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-            SMI_TRY(interior(s));
+#ifdef SMI_LOOPBACK_REHEARSAL
+            if (getenv("SMI_INTERIOR_FIRST")) {  // experiment: enqueue the interior before the ring
+                SMI_TRY(interior(s));
+                SMI_TRY(ring(cs));
+                SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
+            } else
+#endif
+            {
+                SMI_TRY(ring(cs));
+                SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
+                SMI_TRY(interior(s));
+            }
             SMI_HIP_CHECK(hipEventRecord(ev_int, s));
             SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
             if (need_xchg) SMI_TRY(xchg(out, cs));
