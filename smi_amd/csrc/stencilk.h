@@ -75,6 +75,9 @@
 #ifndef SMI_SWEEPK_TASK_ORDER
 #define SMI_SWEEPK_TASK_ORDER 0
 #endif
+#ifndef SMI_SWEEPK_ALT
+#define SMI_SWEEPK_ALT 0
+#endif
 
 namespace smi {
 
@@ -121,7 +124,13 @@ __device__ __forceinline__ void static_for(F &&f) {
 // strip holding column 0, bit 1 for the one holding column Y-1 (both only
 // when one window spans the whole tile); every other wave runs the plain
 // 12-instruction step.
-enum { ROW_NONE = 0, ROW_TOP = 1, ROW_BOT = 2, ROW_FULL = 3 };
+enum { ROW_NONE = 0, ROW_TOP = 1, ROW_BOT = 2, ROW_FULL = 3, ROW_UP = 4 };
+// ROW_UP: a ROW_NONE block that walks upwards (alternating walk directions,
+// SMI_SWEEPK_ALT): row block rb walks down for even rb and up for odd rb, so
+// the 2K apron rows two neighbouring blocks share are read by both at the
+// same time (the ends of both walks, or the starts of both) and the second
+// read hits L2.  Needs an even number of row blocks (launch_sweepk_ex).
+__host__ __device__ constexpr bool walks_up(int row) { return row == ROW_BOT || row == ROW_UP; }
 
 template <int K, int U>
 struct SweepK {
@@ -208,7 +217,7 @@ struct SweepK {
     // row (N) and input t the lower (S); walking up they swap.
     template <int ROW, int CE, bool SC, int PH>
     __device__ __forceinline__ float4 level(int l, int t, const float4 (&P)[3]) const {
-        if constexpr (ROW == ROW_BOT)
+        if constexpr (walks_up(ROW))
             return step<ROW, CE, SC>(r_begin - (t - l), P[PH], P[(PH + 2) % 3], P[(PH + 1) % 3]);
         else
             return step<ROW, CE, SC>(r_begin + t - l, P[(PH + 1) % 3], P[(PH + 2) % 3], P[PH]);
@@ -238,7 +247,7 @@ struct SweepK {
             v = level<ROW, CE, SC, PH>(l, t, W[l - 1]);
             if constexpr (l < K) W[l][PH] = v;
         });
-        store_row<ROW == ROW_BOT, SC>(t, v);
+        store_row<walks_up(ROW), SC>(t, v);
     }
 
     // Branch-free predicated store of the level-K row produced by input t:
@@ -271,7 +280,7 @@ struct SweepK {
     // walks the block again with SC = false.
     template <int ROW, int CE, bool SC>
     __device__ __forceinline__ bool run() {
-        constexpr bool REV = ROW == ROW_BOT;
+        constexpr bool REV = walks_up(ROW);
         emin = 0;
         emax = 0;
         // prologue: input rows 0 .. 2K, compile-time indices; level l starts
@@ -393,7 +402,10 @@ __global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, 
         row = ROW_BOT;
     else if (touchT || touchB)
         row = ROW_FULL;
-    w.r_begin = row == ROW_BOT ? w.o1 - 1 + K : w.o0 - K;
+#if SMI_SWEEPK_ALT
+    if (row == ROW_NONE && (rb & 1)) row = ROW_UP;
+#endif
+    w.r_begin = walks_up(row) ? w.o1 - 1 + K : w.o0 - K;
     switch (row * 4 + ce) {
     case 0: w.template go<ROW_NONE, 0>(); break;
     case 1: w.template go<ROW_NONE, 1>(); break;
@@ -407,6 +419,12 @@ __global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, 
     case 9: w.template go<ROW_BOT, 1>(); break;
     case 10: w.template go<ROW_BOT, 2>(); break;
     case 11: w.template go<ROW_BOT, 3>(); break;
+#if SMI_SWEEPK_ALT
+    case 16: w.template go<ROW_UP, 0>(); break;
+    case 17: w.template go<ROW_UP, 1>(); break;
+    case 18: w.template go<ROW_UP, 2>(); break;
+    case 19: w.template go<ROW_UP, 3>(); break;
+#endif
     default: w.template go<ROW_FULL, 3>(); break;
     }
 }

@@ -96,6 +96,9 @@ int main(int argc, char **argv) {
 #ifdef SB_EVEN_NRB
     nrb += nrb & 1;  // alternating walks: first block down, last block up
 #endif
+#ifdef SB_EVEN_NRB_DOWN
+    if (nrb > 1) nrb -= nrb & 1;  // even, and never more waves than one round
+#endif
     const int blocks = (int)(((long)nstrips * nrb + 3) / 4);
     // timing ping-pongs between the two buffers like a real run (reading the
     // same input every launch would let the 256 MB MALL hold part of it)
