@@ -443,3 +443,22 @@ def test_scaled_guard_mixed_blocks(gpu, oracle_mod, pxpy):
 def test_scaled_guard_every_k(gpu, oracle_mod, k):
     g = _guard_grid(700, 1028, seed=k)
     assert np.array_equal(bits(_run_fused(g, 2 * k + 1, k=k)), bits(oracle_mod.stencil(g, 2 * k + 1)))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_scaled_guard_fuzz(gpu, oracle_mod, seed):
+    """Random tiles whose magnitudes span 2^-135 .. 2^110 with mixed signs and
+    zeros, in patches, so that within one pass some waves stay in the scaled
+    range and others re-walk their blocks exactly; every K, bit-exact."""
+    rng = np.random.default_rng(100 + seed)
+    X, Y = int(rng.integers(60, 400)), 4 * int(rng.integers(20, 200))
+    k = int(rng.integers(3, 13))
+    g = rng.random((X, Y), dtype=np.float32)
+    for _ in range(int(rng.integers(1, 6))):  # patches of scaled magnitudes
+        r0, c0 = int(rng.integers(0, X)), int(rng.integers(0, Y))
+        h, w = int(rng.integers(1, 40)), int(rng.integers(1, 80))
+        e = rng.integers(-135, 111, size=(min(h, X - r0), min(w, Y - c0)))
+        sgn = rng.choice(np.array([-1.0, 1.0, 0.0], np.float32), size=e.shape, p=[0.45, 0.45, 0.1])
+        g[r0:r0 + h, c0:c0 + w] = (sgn * np.ldexp(rng.random(e.shape) + 0.5, e)).astype(np.float32)
+    T = int(rng.integers(k, 3 * k + 2))
+    assert np.array_equal(bits(_run_fused(g, T, k=k)), bits(oracle_mod.stencil(g, T))), (X, Y, k, T)
