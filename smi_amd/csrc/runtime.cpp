@@ -94,11 +94,16 @@ struct ProfRec {
     int tag;
     double units;
     hipEvent_t a, b;
+    bool owns_a;  // false: `a` is the previous record's `b` (chained)
 };
 static std::mutex g_prof_mu;
 static bool g_prof_on = false;
 static std::vector<ProfRec> g_prof_recs;
 static std::vector<hipEvent_t> g_prof_pool;
+// the last record's end marker, while nothing else has been recorded since:
+// a chained begin on the same stream reuses it instead of recording another
+static int g_prof_last = -1;
+static hipStream_t g_prof_last_stream = nullptr;
 
 bool prof_enabled() { return g_prof_on; }
 
@@ -115,23 +120,36 @@ static int prof_get_event(hipEvent_t *e) {
     return SMI_SUCCESS;
 }
 
-int prof_begin(int kernel, hipStream_t stream, int *token, int tag, double units) {
+// chain = true: the caller enqueued nothing on `stream` since the previous
+// prof_end on it (back-to-back passes), so that end marker is this launch's
+// begin -- one marker per launch instead of two (the markers cost ~2 us each
+// between back-to-back 0.11 ms sweeps, 4 % of a 200-pass run with two).
+int prof_begin(int kernel, hipStream_t stream, int *token, int tag, double units, bool chain) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     ProfRec r;
     r.kernel = kernel;
     r.tag = tag;
     r.units = units;
-    SMI_TRY(prof_get_event(&r.a));
+    if (chain && g_prof_last >= 0 && g_prof_last_stream == stream) {
+        r.a = g_prof_recs[g_prof_last].b;
+        r.owns_a = false;
+    } else {
+        SMI_TRY(prof_get_event(&r.a));
+        r.owns_a = true;
+        SMI_HIP_CHECK(hipEventRecord(r.a, stream));
+    }
     SMI_TRY(prof_get_event(&r.b));
-    SMI_HIP_CHECK(hipEventRecord(r.a, stream));
     *token = (int)g_prof_recs.size();
     g_prof_recs.push_back(r);
+    g_prof_last = -1;
     return SMI_SUCCESS;
 }
 
 int prof_end(int token, hipStream_t stream) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     SMI_HIP_CHECK(hipEventRecord(g_prof_recs[token].b, stream));
+    g_prof_last = token;
+    g_prof_last_stream = stream;
     return SMI_SUCCESS;
 }
 
@@ -235,10 +253,11 @@ int smi_prof_reset(void) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     for (auto &r : g_prof_recs) {
         SMI_HIP_CHECK(hipEventSynchronize(r.b));
-        g_prof_pool.push_back(r.a);
+        if (r.owns_a) g_prof_pool.push_back(r.a);
         g_prof_pool.push_back(r.b);
     }
     g_prof_recs.clear();
+    g_prof_last = -1;
     return SMI_SUCCESS;
 }
 

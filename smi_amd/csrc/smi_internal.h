@@ -132,7 +132,7 @@ bool prof_enabled();
 // Bracket one launch: call before (returns a token) and after the launch.
 // tag distinguishes variants of one kernel (the K of a K-step sweep); units
 // is the launch's algorithmic work (cell-steps for the stencil kernels).
-int prof_begin(int kernel, hipStream_t stream, int *token, int tag = 0, double units = 0.0);
+int prof_begin(int kernel, hipStream_t stream, int *token, int tag = 0, double units = 0.0, bool chain = false);
 int prof_end(int token, hipStream_t stream);
 
 size_t type_size(int type);

@@ -84,8 +84,12 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
     int tok = -1;
+    // chained markers for single-tile passes: smi_stencil_run enqueues them
+    // back to back with nothing in between on the stream
+    const bool single_tile = a.gT && a.gB && a.gL && a.gR;
     if (prof && prof_enabled())
-        SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K));
+        SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K,
+                           single_tile));
     int rc = SMI_SUCCESS;
     switch (K) {
     case 3: rc = sweepk_launch_k3(a, nstrips, nrb, blocks, s); break;
