@@ -145,6 +145,13 @@ int prof_begin(int kernel, hipStream_t stream, int *token, int tag, double units
     return SMI_SUCCESS;
 }
 
+// the next prof_begin records its own marker (a caller's own work may
+// follow the last one on the stream)
+void prof_break_chain() {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_last = -1;
+}
+
 int prof_end(int token, hipStream_t stream) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     SMI_HIP_CHECK(hipEventRecord(g_prof_recs[token].b, stream));

@@ -134,6 +134,7 @@ bool prof_enabled();
 // is the launch's algorithmic work (cell-steps for the stencil kernels).
 int prof_begin(int kernel, hipStream_t stream, int *token, int tag = 0, double units = 0.0, bool chain = false);
 int prof_end(int token, hipStream_t stream);
+void prof_break_chain();
 
 size_t type_size(int type);
 

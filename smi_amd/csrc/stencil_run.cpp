@@ -330,6 +330,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
 
     const Plan plan = make_plan(rows, cols, timesteps, side_mask != 0);
     *result_index = plan.passes() & 1;
+    prof_break_chain();  // markers chain only between this run's own passes
     if (timesteps == 0) return SMI_SUCCESS;
     int kmax = 0;  // deepest K-step phase (sizes the depth-K staging)
     for (int i = 0; i < plan.nph; ++i) kmax = std::max(kmax, plan.k[i] >= SWEEPK_MIN ? plan.k[i] : 0);
