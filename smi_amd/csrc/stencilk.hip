@@ -84,12 +84,13 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
     int tok = -1;
-    // chained markers for single-tile passes: smi_stencil_run enqueues them
-    // back to back with nothing in between on the stream
-    const bool single_tile = a.gT && a.gB && a.gL && a.gR;
+    // chained markers: within one smi_stencil_run (which restarts the chain)
+    // the sweeps on this stream follow each other with nothing but event
+    // waits in between (multi-rank: the wait for the previous pass's ring),
+    // so each pass is timed from the end of the previous one
     if (prof && prof_enabled())
         SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K,
-                           single_tile));
+                           true));
     int rc = SMI_SUCCESS;
     switch (K) {
     case 3: rc = sweepk_launch_k3(a, nstrips, nrb, blocks, s); break;
