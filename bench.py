@@ -14,8 +14,9 @@ a barrier + device synchronize on both sides; the time is the max over ranks.
 
 A run of T steps is planned as ceil(T / 12) sweep passes of at most 12 steps,
 balanced to within one step when T % 12 >= 3 (e.g. 20 = 10 + 10; config.plan).  Before the timed
-region every kernel of that plan launches once and untimed K-step passes run
-for at least --warmup-ms (GPU clock settling).
+region every kernel of that plan launches once and untimed runs of the same
+plan repeat for at least --warmup-ms (GPU clock settling; with N > 1 every rank
+runs the same number of them).
 
 The JSON line also carries:
   roofline      -- the stencil kernel with the largest measured time in the
@@ -479,7 +480,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=2400)
     ap.add_argument("--tile", type=int, default=TILE)
     ap.add_argument("--warmup-ms", type=float, default=WARMUP_MS,
-                    help="untimed warm-up floor in ms of K-step passes after the --warmup steps")
+                    help="untimed warm-up floor in ms (repeated runs of the timed plan) after the --warmup steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aux", action="store_true",
                     help="skip the gesummv / reduce / bcast lines measured after the timed stencil region")
@@ -554,11 +555,22 @@ def main() -> None:
         profiling.reset()
         # ... and the GPU clock needs tens of ms of load to settle (120 steps
         # after 10 warm-up steps read ~11 % low, profiles/r01f/
-        # bench_warmup_sweep.log): untimed K-step passes until at least
-        # --warmup-ms of warm-up has run
+        # bench_warmup_sweep.log): untimed runs until at least --warmup-ms of
+        # warm-up has run.  Every rank must run the same number of warm-up runs (each carries
+        # halo exchanges that pair up across ranks): with N > 1 the ranks
+        # agree after every run whether any of them still needs warm-up.
+        # The warm-up runs the timed plan itself, so the kernels the timed
+        # region launches are the ones warmed up (code and clocks).
         t_w = time.perf_counter()
-        while (time.perf_counter() - t_w) * 1e3 < args.warmup_ms:
-            stencil.run(comm, tile, max(K, 1) * 4, PX, PY, scratch)
+        while True:
+            more = (time.perf_counter() - t_w) * 1e3 < args.warmup_ms
+            if world > 1:
+                flag = torch.tensor([1 if more else 0])
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                more = bool(flag.item())
+            if not more:
+                break
+            stencil.run(comm, tile, args.steps if args.steps > 0 else max(K, 1) * 4, PX, PY, scratch)
             torch.cuda.synchronize()
         warm_ms = (time.perf_counter() - t_w) * 1e3
         log(f"warm-up floor done ({warm_ms:.1f} ms)")
