@@ -20,8 +20,9 @@ runs the same number of them).
 
 The JSON line also carries:
   roofline      -- the stencil kernel with the largest measured time in the
-                   timed region (HIP events around every launch, on the launch
-                   stream) and every kernel's share of the region: algorithmic
+                   timed region (HIP events on the launch stream: one marker
+                   between back-to-back passes, so each launch is timed from the
+                   end of the previous one) and every kernel's share of the region: algorithmic
                    8 B/cell/step x cells x K per launch divided by its average
                    duration, vs the 8 TB/s HBM3E peak -- above 1 because of
                    temporal blocking; `traffic` is the HBM bytes per launch
@@ -677,7 +678,7 @@ def main() -> None:
                          "algorithmic_GBs": round(k["algorithmic_GBs"], 1) if k["algorithmic_GBs"] else None}
                         for k in kernels],
             "note": "kernel = the stencil kernel with the largest measured time in the timed region (HIP events "
-                    "around every launch, on its stream); achieved = algorithmic 8 B/cell/step x steps per launch "
+                    "on its stream, one marker between back-to-back passes); achieved = algorithmic 8 B/cell/step x steps per launch "
                     "/ its avg launch time; frac > 1 is temporal blocking: K steps per pass over HBM. traffic = "
                     "measured HBM bytes per launch of that kernel (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                     "profiles/pmc_stencil_sweep.json); hbm_frac = traffic / avg launch time / peak is the memory "
