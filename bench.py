@@ -1,8 +1,18 @@
 #!/usr/bin/env python3
 """bench.py -- stencil_smi Jacobi GCell/s on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--fake-host]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+With N > 1 and no WORLD_SIZE in the environment, bench.py launches its own
+ranks (the reference runs `mpirun -np 8 ./stencil_smi_host`, README.md:96):
+the parent starts N child processes of itself with subprocess before anything
+touches the GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in
+their environment; it never execs), forwards rank 0's result line, and exits
+non-zero if a child fails or outlives --launch-timeout.  --fake-host (implied
+when fewer GPUs than ranks are visible) puts every rank on GPU 0 with its own
+NCCL_HOSTID, so RCCL moves the halos over its socket transport: a functional
+rehearsal of the multi-process path on a one-GPU box, timings meaningless.
 
 A "step" is one Jacobi timestep over the whole job's grid.  N=1 runs
 BASELINE config 2 (8192x8192 fp32 on one GPU, no halo exchange).  N>1 runs
@@ -64,6 +74,10 @@ BYTES_PER_CELL = 8             # one fp32 read + one fp32 write per cell per ste
 TILE = 8192                    # per-GPU tile edge (BASELINE config 2 / weak scaling)
 DECOMP = {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_stencil_sweep.json")
+# rocprofv3 --kernel-trace --stats of the driver's own command, summarised by
+# tools/rocprof_summary.py (kernel -> avg duration), cited next to the line's
+# own HIP-event timing of the same kernel
+ROCPROF_FILE = os.path.join(ROOT, "profiles", "rocprof_driver_cmd.json")
 XGMI_LINK_GBS = 153.6          # MI355X Infinity Fabric: 7 links x 153.6 GB/s per GPU
 GESUMMV_N = 32768              # BASELINE config 5
 COLL_BYTES = (4 << 10, 1 << 20, 64 << 20, 256 << 20)   # BASELINE config 4 span
@@ -79,7 +93,7 @@ def kernel_label(kind: int, tag: int) -> str:
         return "sweep2_kernel (smi_amd/csrc/stencil2.hip, two Jacobi steps per launch)"
     if kind == profiling.SWEEP:
         return "sweep_kernel (smi_amd/csrc/stencil.hip, one Jacobi step per launch)"
-    return "ring kernels (halo-facing band: ringk/ring2/edge)"
+    return "halo-band kernels (bandk_kernel<K> in smi_amd/csrc/stencil_bandk.h, ring2, edge)"
 
 
 def decomposition(n: int) -> tuple[int, int]:
@@ -135,9 +149,12 @@ def cpu_baseline(budget_s: float = 2.0) -> dict:
       legs.serial_reference_order -- the host Reference() loop order
                      (examples/host/stencil_smi.cpp:33-46) on 1 core;
       legs.emulator_config1 / emulator_2x4 -- the rank-decomposed program
-                     (Read/Stencil/Write per rank, halo queues: the threads-
-                     as-ranks emulator semantics) for config 1 (256^2, 2x2,
-                     T=32) and a 2x4 grid of 256^2 tiles, 1 core."""
+                     (Read/Stencil/Write per rank, halo queues) run
+                     threads-as-ranks, one thread per rank (the reference runs
+                     one MPI process per rank, README.md:84-97): config 1
+                     (256^2, 2x2, T=32, 4 threads) and a 2x4 grid of 1024^2
+                     tiles (8 threads); the same program on 1 core beside
+                     each."""
     import oracle
     cpu = host_cpu()
     threads = cpu["threads"]
@@ -164,27 +181,38 @@ def cpu_baseline(budget_s: float = 2.0) -> dict:
     legs["serial_reference_order"] = {
         "GCells": round(2048 * 2048 * 2 * reps / dt / 1e9, 4), "cores": 1,
         "sample": f"2048x2048, {2 * reps} steps in {dt:.2f} s, host Reference() order (stencil_smi.cpp:33-46)"}
-    for name, (X, Y, PX, PY) in (("emulator_config1", (256, 256, 2, 2)), ("emulator_2x4", (512, 1024, 2, 4))):
+    for name, (X, Y, PX, PY) in (("emulator_config1", (256, 256, 2, 2)), ("emulator_2x4", (2048, 4096, 2, 4))):
         ge = oracle.init_uniform(X, Y, seed=5)
-        reps, dt = _time_loop(lambda: oracle.stencil_decomposed(ge, 32, PX, PY), 0.5, 3)
-        legs[name] = {"GCells": round(X * Y * 32 * reps / dt / 1e9, 4), "ms_per_program": round(dt / reps * 1e3, 3),
-                      "cores": 1, "sample": f"{X}x{Y} as {PX}x{PY} ranks of {X // PX}x{Y // PY}, 32 steps, "
-                                            f"{reps} programs"}
+        leg = {"sample": f"{X}x{Y} as {PX}x{PY} ranks of {X // PX}x{Y // PY}, 32 steps", "ranks": PX * PY}
+        for thr in (PX * PY, 1):
+            reps, dt = _time_loop(lambda: oracle.stencil_decomposed(ge, 32, PX, PY, threads=thr), 0.5, 3)
+            key = "threads_as_ranks" if thr > 1 else "one_core"
+            leg[key] = {"GCells": round(X * Y * 32 * reps / dt / 1e9, 4), "ms_per_program": round(dt / reps * 1e3, 3),
+                        "threads": thr, "programs": reps}
+        legs[name] = leg
     out["legs"] = legs
     return out
 
 
 def cpu_aux_legs(budget_s: float = 1.0) -> dict:
-    """CPU legs of the auxiliary configs on the oracle: the canonical reduce
-    fold (reduce.cl:42-148) of 8 contributions, and one 8-way gesummv row
-    shard (4096 x 32768, gesummv_rank0.cl:53-203) on every host thread."""
+    """CPU legs of the auxiliary configs on the oracle, threads-as-ranks
+    (SURVEY §8(d)): the canonical reduce fold (reduce.cl:42-148) of 8
+    contributions folded as 8 owner chunks on 8 threads, the broadcast
+    (bcast.cl:3-111) of one rank's buffer into 7 others packet by packet on 8
+    threads, and one 8-way gesummv row shard (4096 x 32768,
+    gesummv_rank0.cl:53-203) on every host thread."""
     import oracle
     cpu = host_cpu()
     n, count = 8, 16 << 20
     c = np.random.default_rng(3).random((n, count), dtype=np.float32)
-    reps, dt = _time_loop(lambda: oracle.reduce(c, 2, 0), budget_s)
-    red = {"GBs": round(4 * (n + 1) * count * reps / dt / 1e9, 3), "cores": 1,
-           "sample": f"{n} x {count} fp32 add, {reps} folds in {dt:.2f} s (algorithmic bytes 4(n+1) per element)"}
+    reps, dt = _time_loop(lambda: oracle.reduce(c, 2, 0, threads=n), budget_s)
+    red = {"GBs": round(4 * (n + 1) * count * reps / dt / 1e9, 3), "cores": n, "threads_as_ranks": n,
+           "sample": f"{n} x {count} fp32 add as {n} owner chunks, {reps} folds in {dt:.2f} s "
+                     f"(algorithmic bytes 4(n+1) per element)"}
+    reps, dt = _time_loop(lambda: oracle.bcast(c, n - 1, threads=n), budget_s)
+    bc = {"GBs": round(4 * count * reps / dt / 1e9, 3), "cores": n, "threads_as_ranks": n,
+          "sample": f"{4 * count >> 20} MiB fp32 from rank {n - 1} to {n - 1} ranks in 28-byte packets, "
+                    f"{reps} broadcasts in {dt:.2f} s (algbw: message bytes / time)"}
     del c
     rows, m = GESUMMV_N // 8, GESUMMV_N
     rng = np.random.default_rng(4)
@@ -194,7 +222,7 @@ def cpu_aux_legs(budget_s: float = 1.0) -> dict:
     reps, dt = _time_loop(lambda: oracle.gesummv(A, B, x, 1.5, 0.5, threads=cpu["threads"]), budget_s)
     gem = {"GBs": round(4 * (2 * rows * m + m + rows) * reps / dt / 1e9, 3), "cores": cpu["threads"],
            "ms": round(dt / reps * 1e3, 3), "sample": f"{rows}x{m} row shard (A and B), {reps} runs"}
-    return {"reduce_fold_f32": red, "gesummv_shard": gem, "kind": "port", **cpu}
+    return {"reduce_fold_f32": red, "bcast_f32": bc, "gesummv_shard": gem, "kind": "port", **cpu}
 
 
 def pmc_traffic(cells: int, steps_per_launch: int) -> float | None:
@@ -206,6 +234,21 @@ def pmc_traffic(cells: int, steps_per_launch: int) -> float | None:
         for e in d.get("entries", [d]):
             if int(e.get("cells", -1)) == cells and int(e.get("steps_per_launch", 1)) == steps_per_launch:
                 return float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def rocprof_avg(kernel_symbol: str) -> dict | None:
+    """The committed rocprofv3 summary's average duration of this kernel (the
+    driver's bench command under --kernel-trace --stats), if present."""
+    try:
+        with open(ROCPROF_FILE) as f:
+            d = json.load(f)
+        k = d["kernels"].get(kernel_symbol)
+        if k:
+            return {"avg_ms": k["avg_ms"], "calls": k["calls"], "command": d.get("command"),
+                    "source": d.get("source")}
     except (OSError, ValueError, KeyError):
         pass
     return None
@@ -471,6 +514,66 @@ def aux_collectives(comm, world: int, rank: int, stream, barrier) -> list:
     return out
 
 
+def launch_ranks(args, argv: list[str]) -> int:
+    """Start `args.gpus` ranks of this script as child processes (never an
+    exec: the parent has not touched the GPU and does not), forward rank 0's
+    JSON line to stdout, return the first failing child's exit code (0 if
+    all succeed).  The children inherit stderr, so their progress lines keep
+    the job visibly alive."""
+    import signal
+    import socket
+    import subprocess
+    n = args.gpus
+    fake = args.fake_host
+    if not fake:
+        import torch  # device_count() does not initialise the GPU on this image
+        if torch.cuda.device_count() < n:
+            fake = True
+            sys.stderr.write(f"[bench] {torch.cuda.device_count()} GPU(s) visible for {n} ranks: --fake-host\n")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK="0" if fake else str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                   SMI_BENCH_SELF_LAUNCH="1")
+        if fake:
+            env.update(NCCL_HOSTID=f"smi-bench-host-{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+                       SMI_BENCH_FAKE_HOST="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True))
+    deadline = time.monotonic() + args.launch_timeout
+    rc = 0
+    out0 = b""
+    try:
+        out0, _ = procs[0].communicate(timeout=max(1.0, deadline - time.monotonic()))
+        for p in procs:
+            p.wait(timeout=max(1.0, deadline - time.monotonic()))
+    except subprocess.TimeoutExpired:
+        sys.stderr.write(f"[bench] ranks outlived --launch-timeout {args.launch_timeout:.0f} s: killed\n")
+        rc = 124
+    for p in procs:  # each child leads its own process group (start_new_session)
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except OSError:
+                pass
+            p.wait()
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    line = next((ln for ln in out0.decode(errors="replace").splitlines() if ln.startswith("{")), None)
+    if line:
+        sys.stdout.write(line + "\n")
+        sys.stdout.flush()
+    elif rc == 0:
+        sys.stderr.write("[bench] rank 0 printed no result line\n")
+        rc = 1
+    return rc
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -485,7 +588,13 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aux", action="store_true",
                     help="skip the gesummv / reduce / bcast lines measured after the timed stencil region")
+    ap.add_argument("--fake-host", action="store_true",
+                    help="self-launched ranks all on GPU 0, one NCCL_HOSTID each (RCCL over sockets)")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="self-launch: kill every rank after this many seconds")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args, sys.argv[1:]))
 
     # stdout carries exactly one line, the result: anything the libraries
     # underneath write there (RCCL's version banner, gloo's connection notes,
@@ -590,25 +699,37 @@ def main() -> None:
     # Every stencil kernel launched in the timed region, with its measured
     # time (HIP events around each launch on its own stream); the roofline
     # prices the one that took the most time.
+    keys = [(kern, tag) for kern, tag in profiling.entries()
+            if kern in (profiling.SWEEP, profiling.SWEEPK, profiling.EDGE)]
+    if world > 1:
+        # ranks can record different kernels (a tile with neighbours on both
+        # sides and no interior left records no sweep): reduce over the union
+        every = [None] * world
+        dist.all_gather_object(every, keys)
+        keys = sorted({tuple(k) for ks in every for k in ks})
     kernels = []
-    for kern, tag in profiling.entries():
-        if kern not in (profiling.SWEEP, profiling.SWEEPK, profiling.EDGE):
-            continue
+    for kern, tag in keys:
         ms, n, units = profiling.read_tag(kern, tag)
         kernels.append({"kernel": kernel_label(kern, tag), "kind": kern, "tag": tag, "launches": n,
                         "total_ms": ms, "cell_steps": units})
-    if world > 1:  # the slowest rank's times, kernel by kernel (same plan on every rank)
-        t = torch.tensor([elapsed] + [k["total_ms"] for k in kernels], dtype=torch.float64)
+    if world > 1:  # the slowest rank's times, kernel by kernel (0 where a rank has none)
+        t = torch.tensor([elapsed] + [k["total_ms"] for k in kernels] + [k["launches"] for k in kernels]
+                         + [k["cell_steps"] for k in kernels], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
+        nk = len(kernels)
         for i, k in enumerate(kernels):
-            k["total_ms"] = float(t[i + 1])
+            k["total_ms"] = float(t[1 + i])
+            k["launches"] = int(t[1 + nk + i])
+            k["cell_steps"] = float(t[1 + 2 * nk + i])
     timed_ms = elapsed * 1e3
     for k in kernels:
         k["avg_ms"] = k["total_ms"] / max(k["launches"], 1)
         k["share_of_timed_region"] = k["total_ms"] / timed_ms
-        k["algorithmic_GBs"] = (BYTES_PER_CELL * k["cell_steps"] / (k["total_ms"] * 1e-3) / 1e9
-                                if k["total_ms"] > 0 and k["cell_steps"] else None)
+        # 8 B per cell-STEP: with K steps per pass this is K x the bytes the
+        # pass moves (temporal blocking) -- a rate, not a fraction of peak
+        k["cell_step_GBs"] = (BYTES_PER_CELL * k["cell_steps"] / (k["total_ms"] * 1e-3) / 1e9
+                              if k["total_ms"] > 0 and k["cell_steps"] else None)
     sweeps = [k for k in kernels if k["kind"] != profiling.EDGE]
     dom = max(sweeps, key=lambda k: k["total_ms"]) if sweeps else None
 
@@ -618,12 +739,15 @@ def main() -> None:
     if dom:
         spl = dom["tag"]  # steps per launch
         cells_launch = int(round(dom["cell_steps"] / max(dom["launches"], 1) / spl))
-        bytes_launch = BYTES_PER_CELL * cells_launch * spl
+        # compulsory bytes of one pass: every cell it stores read once and
+        # written once (8 B), whatever the steps per pass
+        bytes_launch = BYTES_PER_CELL * cells_launch
         sweep_avg_ms = dom["avg_ms"]
         achieved = bytes_launch / (sweep_avg_ms * 1e-3) / 1e9
+        step_gbs = achieved * spl
         kernel_name = dom["kernel"]
     else:
-        spl, cells_launch, bytes_launch, sweep_avg_ms, achieved, kernel_name = 0, 0, 0, 0.0, 0.0, None
+        spl, cells_launch, bytes_launch, sweep_avg_ms, achieved, step_gbs, kernel_name = 0, 0, 0, 0.0, 0.0, 0.0, None
     traffic = pmc_traffic(cells_per_gpu, spl) if dom else None
     traffic_basis = "measured (rocprofv3 PMC, this tile and kernel)" if traffic else None
     if traffic and world > 1 and cells_launch:
@@ -655,6 +779,9 @@ def main() -> None:
             "plan": [{"steps_per_pass": k, "passes": n} for k, n in plan["phases"]],
             "tuning": stencil.get_tuning(),
             "fusion": fusion,
+            "launch": "self (bench.py started the ranks)" if os.environ.get("SMI_BENCH_SELF_LAUNCH")
+                      else "external" if world > 1 else "single process",
+            "fake_host": bool(os.environ.get("SMI_BENCH_FAKE_HOST")),
             "warmup_ms_floor": args.warmup_ms,
             "warmup_ms_run": round(warm_ms, 1),
         },
@@ -672,19 +799,26 @@ def main() -> None:
             "steps_per_launch": spl,
             "cells_per_launch": cells_launch,
             "bytes_per_launch": int(bytes_launch),
+            "cell_step_GBs": round(step_gbs, 1),
             "share_of_timed_region": round(dom["share_of_timed_region"], 4) if dom else None,
             "kernels": [{"kernel": k["kernel"], "launches": k["launches"], "total_ms": round(k["total_ms"], 5),
                          "avg_ms": round(k["avg_ms"], 5), "share_of_timed_region": round(k["share_of_timed_region"], 4),
-                         "algorithmic_GBs": round(k["algorithmic_GBs"], 1) if k["algorithmic_GBs"] else None}
+                         "cell_step_GBs": round(k["cell_step_GBs"], 1) if k["cell_step_GBs"] else None}
                         for k in kernels],
             "note": "kernel = the stencil kernel with the largest measured time in the timed region (HIP events "
-                    "on its stream, one marker between back-to-back passes); achieved = algorithmic 8 B/cell/step x steps per launch "
-                    "/ its avg launch time; frac > 1 is temporal blocking: K steps per pass over HBM. traffic = "
-                    "measured HBM bytes per launch of that kernel (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
-                    "profiles/pmc_stencil_sweep.json); hbm_frac = traffic / avg launch time / peak is the memory "
-                    "system's utilisation",
+                    "on its stream, one marker between back-to-back passes). achieved = the pass's compulsory "
+                    "bytes (every cell it stores read once + written once, 8 B) / its avg launch time, frac = "
+                    "achieved / peak. traffic = measured HBM bytes per launch of that kernel (rocprofv3 FETCH_SIZE "
+                    "x2 + WRITE_SIZE, profiles/pmc_stencil_sweep.json), hbm_frac = traffic / avg launch time / "
+                    "peak (what the memory system moved, over-fetch included). cell_step_GBs = 8 B per cell-STEP "
+                    "x K steps per pass / launch time: temporal blocking, not a fraction of peak",
         },
     }
+    if dom:
+        rp = rocprof_avg(f"sweepk_kernel<{spl}>") if dom["kind"] == profiling.SWEEPK else None
+        if rp:
+            rp["ratio_to_hip_events"] = round(rp["avg_ms"] / sweep_avg_ms, 4) if sweep_avg_ms else None
+            out["roofline"]["rocprof"] = rp
     if traffic and sweep_avg_ms:
         hbm = traffic / (sweep_avg_ms * 1e-3) / 1e9
         out["roofline"]["hbm_achieved"] = round(hbm, 1)

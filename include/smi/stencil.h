@@ -69,10 +69,10 @@ int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
 
 /* Temporal blocking: steps_per_pass = K in 1..12 fuses up to K Jacobi steps
  * into one pass over HBM (same per-cell arithmetic, bit-identical result).
- * Multi-rank runs then exchange depth-K halos -- K rows/columns per side
- * neighbour and a K x K corner block per diagonal neighbour -- once per K
- * steps; a ring kernel computes the K-wide halo-facing band while the
- * interior sweep runs.  Default K = 12.  A run is planned as K-step passes;
+ * Multi-rank runs then exchange depth-K halos -- K rows / KC = 4 ceil(K/4)
+ * columns per side neighbour and a K x KC corner block per diagonal
+ * neighbour -- once per K steps; a band kernel computes the halo-facing bands
+ * (K rows / KC columns deep) while the interior sweep runs.  Default K = 12.  A run is planned as K-step passes;
  * a remainder r = timesteps % K >= 3 is spread over ceil(timesteps / K)
  * passes balanced to within one step (20 = 10 + 10), r = 1 or 2 adds a pair
  * and/or a single step (smi_stencil_plan).  In a multi-rank run K is
@@ -83,6 +83,15 @@ int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
  * tunes the two-step kernel and is ignored for K >= 3.  Pass 0 to keep. */
 int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_flight);
 int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in_flight);
+
+/* Multi-rank K-step passes: band_rows = output rows per left/right band
+ * sub-window of the band kernel (each walks band_rows + 2K rows; 0 =
+ * automatic, 2K), interior_rounds = rounds of resident waves the interior
+ * sweep is cut into (default 2: workgroups retire mid-pass, so the comm
+ * stream's band kernel and RCCL kernels find slots).  Pass < 0 to keep.
+ * Scheduling only: bit-identical results for every setting. */
+int smi_stencil_set_bands(int band_rows, int interior_rounds);
+int smi_stencil_get_bands(int *band_rows, int *interior_rounds);
 
 /* One phase of a planned run: `passes` launches of `steps_per_pass` steps. */
 typedef struct {

@@ -69,8 +69,9 @@ def lib() -> ctypes.CDLL:
         P = ctypes.c_void_p
         I = ctypes.c_int
         _lib.oracle_stencil.argtypes = [P, P, I, I, I, I, I]
-        _lib.oracle_stencil_decomposed.argtypes = [P, P, I, I, I, I, I]
-        _lib.oracle_reduce.argtypes = [P, P, I, ctypes.c_long, I, I, P]
+        _lib.oracle_stencil_decomposed.argtypes = [P, P, I, I, I, I, I, I]
+        _lib.oracle_reduce.argtypes = [P, P, I, ctypes.c_long, I, I, P, I]
+        _lib.oracle_bcast.argtypes = [P, I, I, ctypes.c_long, I]
         _lib.oracle_gesummv.argtypes = [P, P, P, P, I, I, ctypes.c_float, ctypes.c_float, I]
         L = ctypes.c_long
         _lib.oracle_kmeans_assign.argtypes = [P, L, I, P, I, I, P]
@@ -79,7 +80,7 @@ def lib() -> ctypes.CDLL:
         _lib.oracle_kmeans_reference_data.argtypes = [I, I, I, P, P, P]
         _lib.oracle_minstd_rand0_10000.argtypes = []
         _lib.oracle_minstd_rand0_10000.restype = ctypes.c_ulong
-        for f in ("oracle_stencil", "oracle_stencil_decomposed", "oracle_reduce",
+        for f in ("oracle_stencil", "oracle_stencil_decomposed", "oracle_reduce", "oracle_bcast",
                   "oracle_gesummv", "oracle_max_threads", "oracle_kmeans_assign",
                   "oracle_kmeans_accumulate", "oracle_kmeans", "oracle_kmeans_reference_data"):
             getattr(_lib, f).restype = ctypes.c_int
@@ -120,13 +121,14 @@ def stencil(grid: np.ndarray, T: int, order: str = "device", threads: int = 0) -
     return out
 
 
-def stencil_decomposed(grid: np.ndarray, T: int, PX: int, PY: int) -> np.ndarray:
+def stencil_decomposed(grid: np.ndarray, T: int, PX: int, PY: int, threads: int = 1) -> np.ndarray:
     """Rank-decomposed emulation of the stencil_smi program (Read/Stencil/
-    Write per rank with halo queues, stencil_smi.cl:20-386)."""
+    Write per rank with halo queues, stencil_smi.cl:20-386); threads > 1 runs
+    the ranks as threads (threads-as-ranks, same bits)."""
     g = np.ascontiguousarray(grid, dtype=np.float32)
     out = np.empty_like(g)
     X, Y = g.shape
-    rc = lib().oracle_stencil_decomposed(_ptr(g), _ptr(out), X, Y, PX, PY, T)
+    rc = lib().oracle_stencil_decomposed(_ptr(g), _ptr(out), X, Y, PX, PY, T, threads)
     if rc:
         raise ValueError(f"oracle_stencil_decomposed rc={rc}")
     return out
@@ -158,9 +160,10 @@ def reference_check(result: np.ndarray, reference: np.ndarray) -> bool:
 
 
 # ----------------------------------------------------------------- reduce --
-def reduce(contribs: np.ndarray, dtype: int, op: int, arrival=None) -> np.ndarray:
+def reduce(contribs: np.ndarray, dtype: int, op: int, arrival=None, threads: int = 1) -> np.ndarray:
     """Root-side reduce fold (codegen/templates/reduce.cl:42-148).
-    contribs: (nranks, count) array, row r = rank r's send buffer."""
+    contribs: (nranks, count) array, row r = rank r's send buffer; threads > 1
+    folds `threads` owner chunks side by side (same bits)."""
     npdt = NP_DTYPE[dtype]
     c = np.ascontiguousarray(contribs, dtype=npdt)
     n, count = c.shape
@@ -170,10 +173,22 @@ def reduce(contribs: np.ndarray, dtype: int, op: int, arrival=None) -> np.ndarra
     if arrival is not None:
         arr = np.ascontiguousarray(arrival, dtype=np.int32)
         arr_ptr = _ptr(arr)
-    rc = lib().oracle_reduce(_ptr(c), _ptr(out), n, count, dtype, op, arr_ptr)
+    rc = lib().oracle_reduce(_ptr(c), _ptr(out), n, count, dtype, op, arr_ptr, threads)
     if rc:
         raise ValueError(f"oracle_reduce rc={rc}")
     return out
+
+
+def bcast(bufs: np.ndarray, root: int, threads: int = 1) -> np.ndarray:
+    """Threads-as-ranks broadcast (codegen/templates/bcast.cl:3-111): row r of
+    `bufs` (nranks, n) is rank r's buffer; every row becomes a copy of row
+    `root`, packet by packet.  In place; returns bufs."""
+    assert bufs.flags.c_contiguous
+    n = bufs.shape[0]
+    rc = lib().oracle_bcast(_ptr(bufs), n, root, bufs.nbytes // n, threads)
+    if rc:
+        raise ValueError(f"oracle_bcast rc={rc}")
+    return bufs
 
 
 def _init_value(dtype: int, op: int):

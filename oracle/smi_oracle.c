@@ -137,22 +137,28 @@ int oracle_stencil(const float *in, float *out, int X, int Y, int T, int order,
  * Every rank keeps its own (X_LOCAL+2) x (Y_LOCAL+2) extended tile; the halo
  * queues are modelled as per-rank buffers filled from the neighbours' Write
  * output of the previous timestep.  The result is recombined with
- * CombineMemory (stencil_smi.cpp:80-93). */
+ * CombineMemory (stencil_smi.cpp:80-93).
+ * threads > 1: threads-as-ranks -- the ranks of a timestep run on `threads`
+ * OpenMP threads (one rank per thread when threads == PX*PY, as the
+ * reference runs one MPI process per rank, README.md:84-97), each with its
+ * own extended tile; the end of each timestep is the barrier at which the
+ * halo queues hand over.  Same bits for every thread count. */
 int oracle_stencil_decomposed(const float *in, float *out, int X, int Y, int PX,
-                              int PY, int T) {
+                              int PY, int T, int threads) {
     if (PX <= 0 || PY <= 0 || X % PX || Y % PY || T < 0) return -1;
     const int XL = X / PX, YL = Y / PY, XE = XL + 2, YE = YL + 2;
     const int R = PX * PY;
     float *tile = (float *)malloc(sizeof(float) * (size_t)R * XL * YL);
     float *next = (float *)malloc(sizeof(float) * (size_t)R * XL * YL);
-    float *ext = (float *)malloc(sizeof(float) * (size_t)XE * YE);
+    const int nthr = threads > 1 ? threads : 1;
+    float *ext_all = (float *)malloc(sizeof(float) * (size_t)XE * YE * nthr);
     /* halo queues: what each rank's Write sent in the previous timestep */
     float *snd_top = (float *)malloc(sizeof(float) * (size_t)R * YL);
     float *snd_bot = (float *)malloc(sizeof(float) * (size_t)R * YL);
     float *snd_lft = (float *)malloc(sizeof(float) * (size_t)R * XL);
     float *snd_rgt = (float *)malloc(sizeof(float) * (size_t)R * XL);
-    if (!tile || !next || !ext || !snd_top || !snd_bot || !snd_lft || !snd_rgt) {
-        free(tile); free(next); free(ext); free(snd_top); free(snd_bot);
+    if (!tile || !next || !ext_all || !snd_top || !snd_bot || !snd_lft || !snd_rgt) {
+        free(tile); free(next); free(ext_all); free(snd_top); free(snd_bot);
         free(snd_lft); free(snd_rgt);
         return -2;
     }
@@ -165,7 +171,13 @@ int oracle_stencil_decomposed(const float *in, float *out, int X, int Y, int PX,
                        sizeof(float) * (size_t)YL);
 
     for (int t = 0; t <= T; ++t) {          /* T+1 passes: t=0 is artificial */
+#pragma omp parallel for num_threads(nthr) schedule(static, 1) if (nthr > 1)
         for (int r = 0; r < R; ++r) {
+#ifdef _OPENMP
+            float *ext = ext_all + (size_t)XE * YE * omp_get_thread_num();
+#else
+            float *ext = ext_all;
+#endif
             const int ipx = r / PY, ipy = r % PY;
             const float *my = tile + (size_t)r * XL * YL;
             float *dst = next + (size_t)r * XL * YL;
@@ -213,6 +225,7 @@ int oracle_stencil_decomposed(const float *in, float *out, int X, int Y, int PX,
             }
         }
         /* Write: tee the halos of this pass (consumed at t+1 if t < T). */
+#pragma omp parallel for num_threads(nthr) schedule(static, 1) if (nthr > 1)
         for (int r = 0; r < R; ++r) {
             const float *d = next + (size_t)r * XL * YL;
             memcpy(snd_top + (size_t)r * YL, d, sizeof(float) * (size_t)YL);
@@ -232,7 +245,7 @@ int oracle_stencil_decomposed(const float *in, float *out, int X, int Y, int PX,
                 memcpy(out + ((size_t)px * XL + x) * Y + (size_t)py * YL,
                        tile + ((size_t)(px * PY + py) * XL + x) * YL,
                        sizeof(float) * (size_t)YL);
-    free(tile); free(next); free(ext);
+    free(tile); free(next); free(ext_all);
     free(snd_top); free(snd_bot); free(snd_lft); free(snd_rgt);
     return 0;
 }
@@ -255,6 +268,7 @@ int oracle_stencil_decomposed(const float *in, float *out, int X, int Y, int PX,
     do {                                                                       \
         const T *src = (const T *)contribs;                                    \
         T *dst = (T *)out;                                                     \
+        _Pragma("omp parallel for num_threads(nthr) schedule(static) if (nthr > 1)") \
         for (long i = 0; i < count; ++i) {                                     \
             T q[(S) + 1];                                                      \
             for (int j = 0; j <= (S); ++j) q[j] = (INIT);                      \
@@ -280,9 +294,13 @@ int oracle_stencil_decomposed(const float *in, float *out, int X, int Y, int PX,
 /* wrapping integer add */
 #define IADD(T, UT) ((T)(UT)((UT)(A) + (UT)(B)))
 
+/* threads > 1: threads-as-ranks -- the elements are cut into `threads`
+ * contiguous owner chunks folded side by side (the owner-chunk schedule of
+ * smi_reduce); every element's fold is the same, so are the bits. */
 int oracle_reduce(const void *contribs, void *out, int nranks, long count,
-                  int dtype, int op, const int *arrival) {
+                  int dtype, int op, const int *arrival, int threads) {
     if (nranks <= 0 || count < 0) return -1;
+    const int nthr = threads > 1 ? threads : 1;
     switch (dtype) {
     case OR_FLOAT:
         if (op == OR_ADD) FOLD_BODY(float, 4, 0.0f, ADD_EXPR(A, B));
@@ -317,6 +335,26 @@ int oracle_reduce(const void *contribs, void *out, int nranks, long count,
     default:
         return -2;
     }
+}
+
+/* Broadcast, threads-as-ranks (codegen/templates/bcast.cl:3-111): the root
+ * packs 28-byte payloads (7 fp32, network_message.h:15-23) and every
+ * non-root rank unpacks each packet into its own buffer; rank r's buffer is
+ * bufs + r * bytes.  A bitwise copy whatever the schedule; `threads` ranks
+ * run side by side (the root's support kernel fans packets out in rank
+ * order, bcast.cl:27-45 -- here each receiving rank pulls them). */
+int oracle_bcast(void *bufs, int nranks, int root, long bytes, int threads) {
+    if (nranks <= 0 || root < 0 || root >= nranks || bytes < 0) return -1;
+    const int nthr = threads > 1 ? threads : 1;
+    const char *src = (const char *)bufs + (size_t)root * bytes;
+#pragma omp parallel for num_threads(nthr) schedule(static, 1) if (nthr > 1)
+    for (int r = 0; r < nranks; ++r) {
+        if (r == root) continue;
+        char *dst = (char *)bufs + (size_t)r * bytes;
+        for (long off = 0; off < bytes; off += 28)
+            memcpy(dst + off, src + off, (size_t)(bytes - off < 28 ? bytes - off : 28));
+    }
+    return 0;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -467,8 +505,8 @@ int oracle_kmeans(const float *pts, long n_total, int ranks, int dims, int clust
                 err = oracle_kmeans_accumulate(mine, per, dims, idx, clusters, sums + (size_t)r * kd,
                                                counts + (size_t)r * clusters);
         }
-        if (!err) err = oracle_reduce(sums, rs, ranks, (long)kd, OR_FLOAT, OR_ADD, NULL);
-        if (!err) err = oracle_reduce(counts, rc, ranks, clusters, OR_INT, OR_ADD, NULL);
+        if (!err) err = oracle_reduce(sums, rs, ranks, (long)kd, OR_FLOAT, OR_ADD, NULL, 1);
+        if (!err) err = oracle_reduce(counts, rc, ranks, clusters, OR_INT, OR_ADD, NULL, 1);
         for (size_t i = 0; i < kd && !err; ++i) centroids[i] = rs[i] / (float)rc[i / dims];
     }
     free(idx);

@@ -33,17 +33,16 @@ CXXFLAGS = [
 # (v_pk_add_f32 on aligned pairs); the SLP vectorizer would pack the
 # shuffled (S+W)/(+E) adds too and pay a register move for each pair.
 FILE_FLAGS = {"stencilk_k": ["-fno-slp-vectorize"]}
-# Build variants: the product library, a bounds-checked diagnostic build, the
-# loopback rehearsal build (tools/rehearsal.py) and timing experiments
-# (tools/sweep_experiment.py), each in its own directory.
+# Build variants, each in its own directory: the product library (no
+# experiment switch is compiled into it), a bounds-checked diagnostic build,
+# the loopback rehearsal build (tools/rehearsal.py: SMI_LOOPBACK* switches)
+# and the experiment build (SMI_FOLD_VARIANT / SMI_GEMV_VARIANT launch
+# variants read from the environment).
 VARIANT_FLAGS = {
     "": [],
     "debug": ["-DSMI_BOUNDS_CHECK"],
     "rehearsal": ["-DSMI_LOOPBACK_REHEARSAL"],
-    "exp_g1": ["-DSMI_SWEEPK_GROUPS=1"],
-    "exp_g3": ["-DSMI_SWEEPK_GROUPS=3"],
-    "exp_nt": ["-DSMI_SWEEPK_LOAD_AUX=2"],
-    "exp_onedir": ["-DSMI_EXP_ONE_DIRECTION"],
+    "experiments": ["-DSMI_EXPERIMENTS"],
 }
 
 

@@ -145,16 +145,20 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldRows rows, T *__restrict_
     }
 }
 
-// Launch variant, SMI_FOLD_VARIANT (experiment switch; unset = 0, the tuned
-// default): bit 0 = cached loads/stores instead of nontemporal, bit 1 = grid
+// Launch variant, SMI_FOLD_VARIANT (experiment build only; the library: 0, the
+// tuned default): bit 0 = cached loads/stores instead of nontemporal, bit 1 = grid
 // capped at 4096 blocks (grid-stride loop), bit 2 = two vectors per thread.
 // 8 x 64 Mi fp32 on one MI355X: cached+capped 4.56 TB/s, default 5.75 TB/s.
 static int fold_variant() {
+#ifdef SMI_EXPERIMENTS  // experiment build only (smi_amd/build.py --experiments)
     static int v = [] {
         const char *e = getenv("SMI_FOLD_VARIANT");
         return e ? atoi(e) : 0;
     }();
     return v;
+#else
+    return 0;
+#endif
 }
 
 template <typename T, int S, int OP, int VPT>

@@ -207,15 +207,19 @@ __global__ __launch_bounds__(64 * kGemvWaves) void gemv_split_kernel(const float
     if (lane == 0) y[row] = HAS_B ? __fadd_rn(accA, accB) : accA;
 }
 
-// Launch variant (experiment switch SMI_GEMV_VARIANT; unset = 0, the default):
+// Launch variant (experiment build only, switch SMI_GEMV_VARIANT; the library: 0, the default):
 // 1 = one wave per row for every shape; row split with 2 = whole-slab
 // passes, 3 = quarter-slab passes (default: half-slab passes).
 static int gemv_variant() {
+#ifdef SMI_EXPERIMENTS  // experiment build only (smi_amd/build.py --experiments)
     static int v = [] {
         const char *e = getenv("SMI_GEMV_VARIANT");
         return e ? atoi(e) : 0;
     }();
     return v;
+#else
+    return 0;
+#endif
 }
 
 template <int H>

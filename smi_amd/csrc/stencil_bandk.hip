@@ -1,0 +1,126 @@
+// stencil_bandk.hip -- host side of the halo-facing bands of a K-step pass
+// (kernel: stencil_bandk.h, one instantiation per K in stencilk_k<K>.hip),
+// the initial depth-K pack, and the rehearsal build's one-kernel exchange.
+#include <cstdlib>
+
+#include "stencil_common.h"
+
+namespace smi {
+
+#define SMI_BANDK_DECL(K) int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s);
+SMI_BANDK_DECL(3)
+SMI_BANDK_DECL(4)
+SMI_BANDK_DECL(5)
+SMI_BANDK_DECL(6)
+SMI_BANDK_DECL(7)
+SMI_BANDK_DECL(8)
+SMI_BANDK_DECL(9)
+SMI_BANDK_DECL(10)
+SMI_BANDK_DECL(11)
+SMI_BANDK_DECL(12)
+
+// Rows per left/right sub-window when not tuned: hb + 2K rows walked, so 2K
+// keeps a side wave's walk at 4K rows, close to a top/bottom wave's 3K.
+static int default_band_rows(int K) { return 2 * K; }
+
+int launch_bandk(int K, BandKArgs a, hipStream_t s) {
+    const int X = a.rows, Y = a.cols;
+    const int LL = (K + 3) / 4;
+    a.kc = kc_of(K);
+    SMI_ARG_CHECK(K >= SWEEPK_MIN && K <= SWEEPK_MAX, "bandk: K must be 3..12");
+    SMI_ARG_CHECK(X >= 2 * K && Y >= 2 * a.kc && Y % 4 == 0, "bandk: tile smaller than 2K x 2KC");
+    a.sw = 256 - 8 * LL;
+    const int nwin = (Y + a.sw - 1) / a.sw;
+    a.rlo = a.has[0] ? K : 0;
+    a.rhi = a.has[1] ? X - K : X;
+    a.hb = g_tune.band_rows > 0 ? g_tune.band_rows : default_band_rows(K);
+    a.nsub = a.rhi > a.rlo ? (a.rhi - a.rlo + a.hb - 1) / a.hb : 0;
+    const int side_waves = (a.nsub + 3) / 4;
+    const int waves_of[4] = {a.has[0] ? nwin : 0, a.has[1] ? nwin : 0, a.has[2] ? side_waves : 0,
+                             a.has[3] ? side_waves : 0};
+    int n = 0;
+    for (int k = 0; k < 4; ++k) {
+        a.first[k] = n;
+        n += waves_of[k];
+    }
+    a.first[4] = n;
+    if (n == 0) return SMI_SUCCESS;
+    int tok = -1;
+    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_EDGE, s, &tok, K));
+    int rc = SMI_SUCCESS;
+    switch (K) {
+    case 3: rc = bandk_launch_k3(a, n, s); break;
+    case 4: rc = bandk_launch_k4(a, n, s); break;
+    case 5: rc = bandk_launch_k5(a, n, s); break;
+    case 6: rc = bandk_launch_k6(a, n, s); break;
+    case 7: rc = bandk_launch_k7(a, n, s); break;
+    case 8: rc = bandk_launch_k8(a, n, s); break;
+    case 9: rc = bandk_launch_k9(a, n, s); break;
+    case 10: rc = bandk_launch_k10(a, n, s); break;
+    case 11: rc = bandk_launch_k11(a, n, s); break;
+    default: rc = bandk_launch_k12(a, n, s); break;
+    }
+    SMI_TRY(rc);
+    if (tok >= 0) SMI_TRY(prof_end(tok, s));
+    return SMI_SUCCESS;
+}
+
+// Initial depth-K sends from the current tile: columns 0..KC-1 and
+// Y-KC..Y-1 packed [row][k], and the four K x KC corner blocks.
+__global__ __launch_bounds__(256) void packk_kernel(const float *in, int X, int Y, int K, int KC, HaloK h) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= X * KC) return;
+    const int p = t / KC, k = t - p * KC;
+    const float *row = in + (size_t)p * Y;
+    const float vl = row[k], vr = row[Y - KC + k];
+    h.send_left[t] = vl;
+    h.send_right[t] = vr;
+    if (p < K) {
+        h.send_corner[0][p * KC + k] = vl;
+        h.send_corner[1][p * KC + k] = vr;
+    }
+    if (p >= X - K) {
+        h.send_corner[2][(p - (X - K)) * KC + k] = vl;
+        h.send_corner[3][(p - (X - K)) * KC + k] = vr;
+    }
+}
+
+int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s) {
+    const int KC = kc_of(K);
+    SMI_ARG_CHECK(cols >= 2 * KC && rows >= K, "packk: tile smaller than 2KC columns");
+    const int n = rows * KC;
+    hipLaunchKernelGGL(packk_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, rows, cols, K, KC, h);
+    SMI_HIP_CHECK(hipGetLastError());
+    return SMI_SUCCESS;
+}
+
+#ifdef SMI_LOOPBACK_REHEARSAL
+// Rehearsal build only: the 8-way loopback exchange as ONE copy kernel (an
+// RCCL send/recv group is one kernel launch too), so tools/rehearsal.py can
+// price the exchange without the in-process transport's per-message events.
+struct CopySegs {
+    const float4 *src[8];
+    float4 *dst[8];
+    int n4[8];
+};
+__global__ __launch_bounds__(256) void multicopy_kernel(CopySegs c, int nseg, int blocks_per_seg) {
+    const int seg = blockIdx.x / blocks_per_seg;
+    if (seg >= nseg) return;
+    const int b = blockIdx.x - seg * blocks_per_seg;
+    for (int i = b * 256 + threadIdx.x; i < c.n4[seg]; i += blocks_per_seg * 256) c.dst[seg][i] = c.src[seg][i];
+}
+int launch_multicopy(const float *const *src, float *const *dst, const size_t *bytes, int nseg, hipStream_t s) {
+    CopySegs c{};
+    for (int i = 0; i < nseg && i < 8; ++i) {
+        c.src[i] = reinterpret_cast<const float4 *>(src[i]);
+        c.dst[i] = reinterpret_cast<float4 *>(dst[i]);
+        c.n4[i] = (int)(bytes[i] / 16);
+    }
+    const int bps = 8;
+    hipLaunchKernelGGL(multicopy_kernel, dim3(bps * nseg), dim3(256), 0, s, c, nseg, bps);
+    SMI_HIP_CHECK(hipGetLastError());
+    return SMI_SUCCESS;
+}
+#endif
+
+}  // namespace smi

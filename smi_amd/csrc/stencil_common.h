@@ -76,7 +76,8 @@ struct Tuning {
     // where workgroups retire, so the RCCL kernel of the exchange is never
     // left without a slot until the interior ends.
     int rounds_multi = 2;
-    int uk = 3;         // rows loaded ahead (K-step sweep: one 3-row register batch, fixed at build time)
+    int band_rows = 0;  // rows per left/right band sub-window (stencil_bandk.h); 0 = automatic
+    int uk = 3;        // rows loaded ahead (K-step sweep: one 3-row register batch, fixed at build time)
 };
 extern Tuning g_tune;
 
@@ -128,56 +129,37 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s);
 int launch_sweepk_ex(int K, const SweepKArgs &a, int ht, int reserve, bool prof, hipStream_t s);
 int sweepk_window_cols(int K);  // output columns per 256-column window
 
-// Depth-K halos (stencil_ringk.hip).  Receive side: top = rows -K..-1 and
-// bot = rows X..X+K-1 (K x Y, row-major), left = cols -K..-1 and right =
-// cols Y..Y+K-1 (X x K, [row][k]), corner[tl,tr,bl,br] = K x K blocks of the
-// diagonal neighbours.  Send side: send_left/right = this tile's cols 0..K-1
-// / Y-K..Y-1 ([row][k]), send_corner = its own four K x K corner blocks.
-// The top/bottom rows are sent straight from the tile.  Every pointer is a
-// valid allocation, also for sides without a neighbour.
+// Depth-K halos (stencil_bandk.h / stencil_bandk.hip).  KC = 4 ceil(K/4):
+// the column depth, whole float4 groups.  Receive side: top = rows -K..-1 and
+// bot = rows X..X+K-1 (K x Y, row-major), left = cols -KC..-1 and right =
+// cols Y..Y+KC-1 (X x KC, [row][k]), corner[tl,tr,bl,br] = K x KC blocks of
+// the diagonal neighbours.  Send side: send_left/right = this tile's cols
+// 0..KC-1 / Y-KC..Y-1 ([row][k]), send_corner = its own four K x KC corner
+// blocks.  The top/bottom rows are sent straight from the tile.  Every
+// pointer is a valid allocation, also for sides without a neighbour.
 struct HaloK {
     const float *top, *bot, *left, *right;
     const float *corner[4];
     float *send_left, *send_right;
     float *send_corner[4];
 };
-constexpr int RING_KMAX = 12;
-constexpr int RB_H = 64;  // ring block rows (left/right bands)
-constexpr int RB_W = 64;  // ring block columns (top/bottom bands)
-struct RingKArgs {
+__host__ __device__ constexpr int kc_of(int K) { return 4 * ((K + 3) / 4); }
+struct BandKArgs {
     const float *in;
     float *out;
-    int rows, cols, k;
-    int bandw;         // left/right band width: K rounded up to float4 columns (set by launch_ringk)
+    int rows, cols;
+    int kc;            // column depth of the side bands / halos / packs: kc_of(K)
     int has[4];        // neighbour on side top, bottom, left, right
-    int has_diag[4];   // neighbour tl, tr, bl, br
-    int band[4];       // compute the band of side k (halo side, or a global edge column)
-    int pack;          // write the next exchange's sends (multi-rank)
+    int pack;          // tee the next exchange's packed columns / corner blocks
     HaloK h;
-    // filled by launch_ringk: band rectangles and block prefix
-    int r0[4], r1[4], c0[4], c1[4];
-    int first_block[5];
-    int exp_mode;      // timing experiments (rehearsal build, SMI_RING_EXP): 1 no levels, 2 no loads, 4 no stores
+    // filled by launch_bandk
+    int first[5];      // first wave of band top, bottom, left, right; first[4] = all waves
+    int sw;            // output columns per top/bottom window
+    int rlo, rhi;      // rows of the left/right bands
+    int hb;            // output rows per left/right sub-window
+    int nsub;          // sub-windows per left/right band
 };
-int launch_ringk(RingKArgs a, hipStream_t s);
-
-// The same halo-facing bands as register sweeps (stencil_bands.hip): the
-// extended-tile rows/columns the bands need are gathered into two small
-// images -- H: the top band's rows [-K, 2K) over [Y + aprons] columns stacked
-// on the bottom band's rows [X-2K, X+K); V: the tile's rows with the left
-// band's columns [-KC, 2KC) beside the right band's [Y-2KC, Y+KC) -- swept by
-// sweepk_kernel<K> with few, tall row blocks, and scattered back into the
-// tile with the next exchange's sends.  About 100 waves in all, so they run
-// beside an interior sweep that leaves them their slots.
-struct BandImages {
-    float *h_in, *h_out;  // 6K x wi
-    float *v_in, *v_out;  // rows x 6KC
-};
-size_t band_images_elems(int rows, int cols, int K);
-bool bands_eligible(int rows, int cols, int K);
-BandImages band_images_at(float *base, int rows, int cols, int K);
-constexpr int BAND_RESERVE_WAVES = 160;  // interior waves left to the band sweeps + exchange
-int launch_ring_bands(const RingKArgs &a, const BandImages &im, hipStream_t s);
+int launch_bandk(int K, BandKArgs a, hipStream_t s);
 int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s);
 #ifdef SMI_LOOPBACK_REHEARSAL
 int launch_multicopy(const float *const *src, float *const *dst, const size_t *bytes, int nseg, hipStream_t s);

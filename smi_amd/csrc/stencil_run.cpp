@@ -95,8 +95,8 @@ static int exchange2(Comm *c, const Neighbours &nb, const float *tile, int rows,
     return grp.end();
 }
 
-// Depth-K exchange (once per K steps): K rows / K columns per side
-// neighbour, one K x K block per diagonal neighbour.
+// Depth-K exchange (once per K steps): K rows / KC = kc_of(K) columns per
+// side neighbour, one K x KC block per diagonal neighbour.
 struct HaloKBuf {
     float *top, *bot, *left, *right, *send_left, *send_right;
     float *corner[4], *send_corner[4];
@@ -120,10 +120,11 @@ static int exchangek(Comm *c, const Neighbours &nb, const float *tile, int rows,
                      hipStream_t s) {
     Transport *tp = c->transport.get();
 #ifdef SMI_LOOPBACK_REHEARSAL
-    if (getenv("SMI_LOOPBACK_NOXCHG")) return SMI_SUCCESS;  // rehearsal: price ring + interior alone
+    if (getenv("SMI_LOOPBACK_NOXCHG")) return SMI_SUCCESS;  // rehearsal: price bands + interior alone
 #endif
-    const size_t rb = (size_t)K * cols * sizeof(float), cb = (size_t)rows * K * sizeof(float);
-    const size_t kb = (size_t)K * K * sizeof(float);
+    const int KC = kc_of(K);
+    const size_t rb = (size_t)K * cols * sizeof(float), cb = (size_t)rows * KC * sizeof(float);
+    const size_t kb = (size_t)K * KC * sizeof(float);
 #ifdef SMI_LOOPBACK_REHEARSAL
     if (getenv("SMI_LOOPBACK_FUSED") && nb.top == 0 && nb.left == 0 && nb.tl == 0) {
         // rehearsal: the same 8 messages as one copy kernel (like one RCCL group)
@@ -274,6 +275,19 @@ int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in
     return SMI_SUCCESS;
 }
 
+int smi_stencil_set_bands(int band_rows, int interior_rounds) {
+    SMI_ARG_CHECK(band_rows <= 65536 && interior_rounds <= 64, "band_rows / interior_rounds out of range");
+    if (band_rows >= 0) g_tune.band_rows = band_rows;
+    if (interior_rounds >= 0) g_tune.rounds_multi = std::max(1, interior_rounds);
+    return SMI_SUCCESS;
+}
+
+int smi_stencil_get_bands(int *band_rows, int *interior_rounds) {
+    if (band_rows) *band_rows = g_tune.band_rows;
+    if (interior_rounds) *interior_rounds = g_tune.rounds_multi;
+    return SMI_SUCCESS;
+}
+
 int smi_stencil_plan(int x_local, int y_local, int px, int py, int rank, int timesteps, SMI_StencilPhase *phases,
                      int max_phases, int *nphases, int *neighbours, int *result_index) {
     SMI_ARG_CHECK(x_local >= 1 && y_local >= 4 && y_local % 4 == 0, "tile must be >= 1 x 4, y_local % 4 == 0");
@@ -317,7 +331,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     // `smi_amd/build.py --rehearsal`, driven by tools/rehearsal.py): with
     // SMI_LOOPBACK=1 a 1x1 run is its own neighbour on every side and
     // diagonal, so one GPU replays the full per-pass work of an interior rank
-    // of a large decomposition (ring kernel, 8-way exchange through the
+    // of a large decomposition (band kernel, 8-way exchange through the
     // transport, interior sweep) with the same stream schedule.  The halos
     // then wrap around, so the numbers differ from the stencil's.
     if (px == 1 && py == 1 && c->size == 1 && getenv("SMI_LOOPBACK"))
@@ -345,9 +359,8 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     a2.cols = cols;
     for (int k = 0; k < 4; ++k) a2.skip[k] = side_nb[k] >= 0;
     // K-step passes: the interior sweep stays K rows / 4*ceil(K/4) columns
-    // clear of every halo-facing side (the ring kernel computes those bands
+    // clear of every halo-facing side (the band kernel computes those bands
     // beside it); global edges are handled inside the sweep (stencilk.h).
-    auto kc_of = [](int K) { return 4 * ((K + 3) / 4); };
     auto interior_args = [&](int K) {
         SweepKArgs ak{};
         ak.rows = rows;
@@ -363,17 +376,13 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
         ak.gR = nb.right < 0;
         return ak;
     };
-    const int diag_nb[4] = {nb.tl, nb.tr, nb.bl, nb.br};
-    auto ring_args = [&](int K) {
-        RingKArgs rk{};
-        rk.rows = rows;
-        rk.cols = cols;
-        rk.k = K;
-        for (int k = 0; k < 4; ++k) rk.has[k] = side_nb[k] >= 0;
-        for (int k = 0; k < 4; ++k) rk.has_diag[k] = diag_nb[k] >= 0;
-        for (int k = 0; k < 4; ++k) rk.band[k] = rk.has[k];
-        rk.pack = side_mask != 0;
-        return rk;
+    auto band_args = [&]() {
+        BandKArgs bk{};
+        bk.rows = rows;
+        bk.cols = cols;
+        for (int k = 0; k < 4; ++k) bk.has[k] = side_nb[k] >= 0;
+        bk.pack = side_mask != 0;
+        return bk;
     };
 
     int cur = 0;  // index of the buffer holding the current state
@@ -408,26 +417,15 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
 
     // Halo staging.  Depth 2 (its inner row/column doubles as the depth-1
     // halo): top2 | bot2 | left2 | right2 | corner(4) | send_left2 |
-    // send_right2 | send_corner(4); then depth K: top | bot (K x cols) | left
-    // | right | send_left | send_right (rows x K, [row][k]) | 4 + 4 K x K
-    // corners.  The regions are sized for the deepest phase; a shallower
-    // phase (the remainder pass) lays its depth out densely from the start
-    // of each region.
-    const size_t need2 = 4 * (size_t)cols + 8 * (size_t)rows + 8;
-    const size_t needk =
-        kmax ? 2 * (size_t)kmax * cols + 4 * (size_t)rows * kmax + 8 * (size_t)kmax * kmax : 0;
-    // Halo-facing bands of the K-step passes: the LDS ring kernel (default),
-    // or -- SMI_RING_MODE=1, an experiment -- register sweeps over gathered
-    // band images (stencil_bands.hip).  Bit-identical either way; the band
-    // sweeps lost on the interior-rank rehearsal (0.50 vs 0.76-0.79 of a lone
-    // tile): their chain of six small kernels is latency-bound under the
-    // interior's saturated HBM (gather 28 -> 74 us, band sweeps 20 + 31 ->
-    // 56 + 66 us when run beside it; profiles/r02/rehearsal/bands_*).
-    const char *rm = getenv("SMI_RING_MODE");
-    const bool bands = kmax && rm && atoi(rm) != 0 && bands_eligible(rows, cols, kmax);
-    const size_t needb = bands ? band_images_elems(rows, cols, kmax) : 0;
-    const size_t offb = (need2 + needk + 3) / 4 * 4;
-    SMI_TRY(ensure_halo(c, offb + needb));
+    // send_right2 | send_corner(4); then depth K (16-byte aligned): top | bot
+    // (K x cols) | left | right | send_left | send_right (rows x KC, [row][k])
+    // | 4 + 4 K x KC corners.  The regions are sized for the deepest phase; a
+    // shallower phase (the remainder pass) lays its depth out densely from
+    // the start of each region.
+    const size_t need2 = (4 * (size_t)cols + 8 * (size_t)rows + 8 + 3) / 4 * 4;
+    const size_t kcmax = kc_of(kmax);
+    const size_t needk = kmax ? 2 * (size_t)kmax * cols + 4 * (size_t)rows * kcmax + 8 * (size_t)kmax * kcmax : 0;
+    SMI_TRY(ensure_halo(c, need2 + needk));
     Halo2Buf hb;
     hb.top2 = c->halo;
     hb.bot2 = hb.top2 + 2 * (size_t)cols;
@@ -444,13 +442,13 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
         hk.top = p;
         hk.bot = hk.top + (size_t)kmax * cols;
         hk.left = hk.bot + (size_t)kmax * cols;
-        hk.right = hk.left + (size_t)rows * kmax;
-        hk.send_left = hk.right + (size_t)rows * kmax;
-        hk.send_right = hk.send_left + (size_t)rows * kmax;
-        float *q = hk.send_right + (size_t)rows * kmax;
+        hk.right = hk.left + (size_t)rows * kcmax;
+        hk.send_left = hk.right + (size_t)rows * kcmax;
+        hk.send_right = hk.send_left + (size_t)rows * kcmax;
+        float *q = hk.send_right + (size_t)rows * kcmax;
         for (int k = 0; k < 4; ++k) {
-            hk.corner[k] = q + (size_t)k * kmax * kmax;
-            hk.send_corner[k] = q + (size_t)(4 + k) * kmax * kmax;
+            hk.corner[k] = q + (size_t)k * kmax * kcmax;
+            hk.send_corner[k] = q + (size_t)(4 + k) * kmax * kcmax;
         }
         return hk;
     };
@@ -495,7 +493,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             // interior's launch -- the trace of an interior rank showed the
             // main stream idle ~100 us per pass behind the exchange calls.
 #ifdef SMI_LOOPBACK_REHEARSAL
-            if (getenv("SMI_INTERIOR_FIRST")) {  // experiment: enqueue the interior before the ring
+            if (getenv("SMI_INTERIOR_FIRST")) {  // experiment: enqueue the interior before the bands
                 SMI_TRY(interior(s));
                 SMI_TRY(ring(cs));
                 SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
@@ -530,28 +528,19 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             const HaloKBuf hk = halok();
             const HaloK hkv = hk.view();
             SweepKArgs ak = interior_args(K);
-            RingKArgs rk = ring_args(K);
-            rk.h = hkv;
+            BandKArgs bk = band_args();
+            bk.h = hkv;
             auto xchgk = [&](const float *tile, hipStream_t st) {
                 return exchangek(c, nb, tile, rows, cols, K, hk, st);
             };
             SMI_TRY(launch_packk(bufp(cur), rows, cols, K, hkv, cs));
             SMI_TRY(xchgk(bufp(cur), cs));
-            const bool use_bands = bands && bands_eligible(rows, cols, K);
-            const BandImages im = use_bands ? band_images_at(c->halo + offb, rows, cols, K) : BandImages{};
             for (int p = 0; p < npass; ++p, cur ^= 1) {
-                rk.in = ak.in = bufp(cur);
-                rk.out = ak.out = bufp(cur ^ 1);
-                if (use_bands)
-                    SMI_TRY(pass([&](hipStream_t st) { return launch_ring_bands(rk, im, st); },
-                                 [&](hipStream_t st) {
-                                     return launch_sweepk_ex(K, ak, 0, overlap ? BAND_RESERVE_WAVES : 0, true, st);
-                                 },
-                                 xchgk, p < npass - 1, ak.out));
-                else
-                    SMI_TRY(pass([&](hipStream_t st) { return launch_ringk(rk, st); },
-                                 [&](hipStream_t st) { return launch_sweepk(K, ak, st); }, xchgk, p < npass - 1,
-                                 ak.out));
+                bk.in = ak.in = bufp(cur);
+                bk.out = ak.out = bufp(cur ^ 1);
+                SMI_TRY(pass([&](hipStream_t st) { return launch_bandk(K, bk, st); },
+                             [&](hipStream_t st) { return launch_sweepk(K, ak, st); }, xchgk, p < npass - 1,
+                             ak.out));
             }
         } else if (K == 2) {
             // ---- pairs of steps (depth-2 halos)

@@ -68,11 +68,7 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
             if (!(a.gT && a.gB && a.gL && a.gR)) waves = std::max(1, waves * atoi(e) / 100);
 #endif
         const bool single = a.gT && a.gB && a.gL && a.gR;
-        int rounds_multi = g_tune.rounds_multi;
-#ifdef SMI_LOOPBACK_REHEARSAL
-        if (const char *e = getenv("SMI_ROUNDS_MULTI")) rounds_multi = atoi(e);
-#endif
-        int rounds = single ? 1 : std::max(1, rounds_multi);
+        int rounds = single ? 1 : std::max(1, g_tune.rounds_multi);
         if (!single && reserve > 0) {
             waves = std::max(64, waves - reserve);
             rounds = 1;

@@ -116,6 +116,19 @@ def get_tuning() -> dict:
                 overlap=v[3].value)
 
 
+def set_bands(band_rows: int = -1, interior_rounds: int = -1) -> None:
+    """Multi-rank K-step scheduling (bit-neutral): rows per left/right band
+    sub-window of the band kernel (0 = automatic) and rounds of resident waves
+    the interior sweep is cut into."""
+    _lib.call("smi_stencil_set_bands", band_rows, interior_rounds)
+
+
+def get_bands() -> dict:
+    v = [ctypes.c_int() for _ in range(2)]
+    _lib.call("smi_stencil_get_bands", *[ctypes.byref(x) for x in v])
+    return dict(band_rows=v[0].value, interior_rounds=v[1].value)
+
+
 def set_fusion(steps_per_pass: int = 0, rows_per_wave: int = 0, rows_in_flight: int = 0) -> None:
     """Up to steps_per_pass (1..12) Jacobi steps fused per pass over HBM
     (same bits for every setting); the remainder of a run is one shallower

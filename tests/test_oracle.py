@@ -120,6 +120,23 @@ def test_stencil_decomposed_equals_full(pxpy):
     full = o.stencil(g, 17)
     dec = o.stencil_decomposed(g, 17, PX, PY)
     assert np.array_equal(full.view(np.uint32), dec.view(np.uint32))
+    # threads-as-ranks (the CPU baseline's emulator legs): same bits
+    thr = o.stencil_decomposed(g, 17, PX, PY, threads=PX * PY)
+    assert np.array_equal(full.view(np.uint32), thr.view(np.uint32))
+
+
+@pytest.mark.parametrize("dtype,op", [(2, 0), (1, 0), (3, 1), (5, 2)])
+def test_reduce_threads_as_ranks_same_bits(dtype, op):
+    rng = np.random.default_rng(dtype * 3 + op)
+    c = (rng.random((8, 10007)) * 200 - 100).astype(o.NP_DTYPE[dtype])
+    assert np.array_equal(o.reduce(c, dtype, op), o.reduce(c, dtype, op, threads=8))
+
+
+def test_bcast_threads_as_ranks_copies_root():
+    b = np.random.default_rng(9).random((8, 1001), dtype=np.float32)   # 4004 B: a partial last packet
+    want = b[5].copy()
+    o.bcast(b, 5, threads=8)
+    assert all(np.array_equal(b[r].view(np.uint32), want.view(np.uint32)) for r in range(8))
 
 
 def test_stencil_order_matters():

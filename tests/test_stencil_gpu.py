@@ -349,6 +349,26 @@ def test_deep_decomposed(gpu, oracle_mod, k, pxpy, overlap):
         assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, pxpy, T)
 
 
+@pytest.mark.parametrize("k", [3, 7, 10, 12])
+@pytest.mark.parametrize("bands", [(1, 1), (5, 2), (24, 3), (1000, 2)])
+def test_band_tuning_is_bit_neutral(gpu, oracle_mod, k, bands):
+    """The band kernel's side sub-window height (1 row .. taller than the
+    tile) and the interior's rounds of resident waves change scheduling only:
+    a 3x3 decomposition (one interior rank with all eight neighbours) stays
+    bit-exact.  K = 7 and 10 have column bands (KC = 8, 12) wider than K."""
+    from smi_amd import stencil
+    band_rows, rounds = bands
+    old = stencil.get_bands()
+    stencil.set_bands(band_rows, rounds)
+    try:
+        g = oracle_mod.init_uniform(3 * 61, 3 * 140, seed=k + band_rows)
+        for T in (k, 2 * k + 1):
+            got = _run_fused(g, T, 3, 3, 1, k=k)
+            assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, bands, T)
+    finally:
+        stencil.set_bands(old["band_rows"], old["interior_rounds"])
+
+
 @pytest.mark.parametrize("k", [4, 8, 12])
 def test_deep_decomposed_small_tiles(gpu, oracle_mod, k):
     # exactly 2K x 2K tiles (smallest deep tile), ring blocks larger than tiles

@@ -1,16 +1,31 @@
 #!/bin/bash
-# band-sweep ring: multi-rank parity (both ring modes) + interior-rank rehearsal (both modes)
+# Band-kernel check on one GPU into gpurun_out/<tag>: the multi-rank stencil
+# parity tests, the bench self-launch test, then the interior-rank rehearsal
+# (tools/rehearsal.py, rehearsal build) with a one-copy-kernel exchange, no
+# exchange, and the in-process transport, and a kernel trace of one rehearsal.
 set -o pipefail
-cd $GRAFT_REPO_ROOT
-O=gpurun_out/$1; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_stencil_gpu.py tests/test_configs_at_size_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "decomposed or config3 or special or guard or halo or remainder or clipped" > $O/tests_bands.log 2>&1 || { tail -30 $O/tests_bands.log; exit 1; }
-tail -1 $O/tests_bands.log
-SMI_RING_MODE=0 timeout -k 10 400 python -u -m pytest tests/test_stencil_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "decomposed or special or guard" > $O/tests_lds.log 2>&1 || { tail -30 $O/tests_lds.log; exit 1; }
-tail -1 $O/tests_lds.log
-for m in 1 0; do
-  SMI_RING_MODE=$m SMI_LOOPBACK_FUSED=1 REHEARSAL_ROUNDS=1,2 timeout -k 10 150 python tools/rehearsal.py 8192 12 > $O/rehearsal_mode$m.jsonl 2>>$O/err.log || exit 1
-  grep '"overlap": 1' $O/rehearsal_mode$m.jsonl | python -c "
-import json,sys
-for l in sys.stdin:
-    d=json.loads(l); print('ring mode $m rounds',d['rounds'],'eff',d['efficiency'],'ring',d['ring_avg_ms'],'int',d['interior_avg_ms'],'alone',d['ms_per_step_alone'],'rank',d['ms_per_step_interior_rank'])"
-done
+R=$GRAFT_REPO_ROOT
+cd $R
+O=gpurun_out/$1
+mkdir -p $O
+step() {  # step <name> <cmd...>: stop at the first failing step
+  echo "=== $1"; shift
+  "$@"; rc=$?
+  if [ $rc -ne 0 ]; then echo "=== FAILED rc=$rc"; exit $rc; fi
+}
+step tests bash -c "timeout -k 10 600 python -u -m pytest tests/test_stencil_gpu.py tests/test_bench_launch_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k '${TESTS_K:-decomposed or band or special or guard or remainder or clipped or config1 or launch}' > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }"
+tail -1 $O/tests.log
+step reh_fused bash -c "SMI_LOOPBACK_FUSED=1 REHEARSAL_ROUNDS=${ROUNDS:-1,2} REHEARSAL_BAND_ROWS=${BAND_ROWS:-0,12,48} REHEARSAL_OVERLAP=1 timeout -k 10 200 python tools/rehearsal.py 8192 12 > $O/rehearsal_fused.jsonl 2>$O/rehearsal.err"
+step reh_noxchg bash -c "SMI_LOOPBACK_NOXCHG=1 REHEARSAL_ROUNDS=${ROUNDS:-1,2} REHEARSAL_OVERLAP=1 timeout -k 10 120 python tools/rehearsal.py 8192 12 > $O/rehearsal_noxchg.jsonl 2>>$O/rehearsal.err"
+step reh_transport bash -c "REHEARSAL_ROUNDS=${ROUNDS:-1,2} REHEARSAL_OVERLAP=1,0 timeout -k 10 150 python tools/rehearsal.py 8192 12 > $O/rehearsal_transport.jsonl 2>>$O/rehearsal.err"
+cd /tmp && export TMPDIR=/tmp
+step trace env SMI_LOOPBACK_FUSED=1 REHEARSAL_ROUNDS=2 REHEARSAL_OVERLAP=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/trace -o run -- python $R/tools/rehearsal.py 8192 12 > $R/$O/trace.log 2>&1
+cd $R
+python - <<PY
+import json
+for f in ("fused", "noxchg", "transport"):
+    for l in open("$O/rehearsal_%s.jsonl" % f):
+        d = json.loads(l)
+        print(f, "rounds", d["rounds"], "band_rows", d["band_rows"], "ov", d["overlap"], "eff", d["efficiency"],
+              "band", d["band_avg_ms"], "int", d["interior_avg_ms"], "alone", d["ms_per_step_alone"])
+PY

@@ -2,6 +2,7 @@
 """Summarise rocprofv3 outputs into profiles/.
 
   pmc_summarize.py kt   <kernel_stats.csv> <out.json>
+  pmc_summarize.py driver <kernel_stats.csv> <command> <out.json>
   pmc_summarize.py pmc  <fetch_counter_collection.csv> <write_counter_collection.csv> <cells> <out.json> [K]
 
 With K >= 3 only the dispatches of sweepk_kernel<K> count, and the result is
@@ -40,6 +41,18 @@ def counter_per_dispatch(path, name, kernel=KERNEL):
 
 def main():
     mode = sys.argv[1]
+    if mode == "driver":
+        # per-kernel averages of a --kernel-trace --stats run of `command`
+        # (bench.py cites them next to its own HIP-event timing)
+        ks = {}
+        for r in rows(sys.argv[2]):
+            name = r["Name"]
+            short = name.split("(")[0].replace("void ", "").replace("smi::", "").strip()
+            ks[short] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) * 1e-6,
+                         "min_ms": float(r["MinNs"]) * 1e-6, "max_ms": float(r["MaxNs"]) * 1e-6,
+                         "total_ms": float(r["TotalDurationNs"]) * 1e-6}
+        json.dump({"command": sys.argv[3], "source": sys.argv[2], "kernels": ks}, open(sys.argv[4], "w"), indent=1)
+        return
     if mode == "kt":
         out = []
         for r in rows(sys.argv[2]):

@@ -4,14 +4,18 @@
 Loads the rehearsal build of the library (smi_amd/build.py --rehearsal,
 SMI_LOOPBACK_REHEARSAL), in which a 1x1 run with SMI_LOOPBACK=1 is its own
 neighbour on all four sides and four diagonals: the GPU then does exactly the
-per-pass work of an interior rank of a large decomposition (ring kernel,
-8-peer exchange through the transport, interior sweep on the main stream)
+per-pass work of an interior rank of a large decomposition (band kernel on
+the comm stream, 8-peer exchange through the transport, interior sweep on the
+main stream)
 with the production stream schedule.  The halos wrap around, so the values
 are not the stencil's -- timing only.  Prints ms/step next to the plain
 single-tile run, i.e. an estimate of per-GPU weak-scaling efficiency with
 an exchange that costs one device-to-device copy of the halo bytes.
-SMI_ROUNDS_MULTI (read by the rehearsal build only) sets how many rounds of
-resident waves the multi-rank interior sweep is cut into.
+REHEARSAL_ROUNDS (list) sets the rounds of resident waves the multi-rank
+interior sweep is cut into, REHEARSAL_BAND_ROWS (list) the rows per side-band
+sub-window of the band kernel (smi_stencil_set_bands; 0 = automatic).
+SMI_LOOPBACK_FUSED=1 prices the exchange as one copy kernel (like one RCCL
+group), SMI_LOOPBACK_NOXCHG=1 leaves it out.
 usage: rehearsal.py [tile] [K...]
 """
 import json
@@ -62,25 +66,27 @@ def main():
         os.environ.pop("SMI_LOOPBACK", None)
         alone = timed(comm, t, sc, steps)[0]
         noxchg = os.environ.get("SMI_LOOPBACK_NOXCHG")
-        for rounds in [int(r) for r in os.environ.get("REHEARSAL_ROUNDS", "1,2,3,4,6").split(",")]:
-            os.environ["SMI_ROUNDS_MULTI"] = str(rounds)
-            for ov in (1, 0):
+        grid = [(r, b) for r in (int(x) for x in os.environ.get("REHEARSAL_ROUNDS", "1,2,3").split(","))
+                for b in (int(x) for x in os.environ.get("REHEARSAL_BAND_ROWS", "0").split(","))]
+        for rounds, band_rows in grid:
+            stencil.set_bands(band_rows, rounds)
+            for ov in [int(x) for x in os.environ.get("REHEARSAL_OVERLAP", "1,0").split(",")]:
                 stencil.set_tuning(overlap=ov)
                 os.environ["SMI_LOOPBACK"] = "1"
                 runs = timed(comm, t, sc, steps)
                 loop = runs[0]
-                ring = profiling.read(profiling.EDGE)
+                band = profiling.read(profiling.EDGE)
                 sweep = profiling.read(profiling.SWEEPK if k >= 4 else profiling.SWEEP)
                 os.environ.pop("SMI_LOOPBACK", None)
-                print(json.dumps({"K": k, "rounds": rounds, "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
+                print(json.dumps({"K": k, "rounds": rounds, "band_rows": band_rows, "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
                                   "ms_per_step_alone": round(alone, 5),
                                   "ms_per_step_interior_rank": round(loop, 5),
                                   "efficiency": round(alone / loop, 4),
                                   "runs_ms_per_step": [round(r, 5) for r in runs],
-                                  "ring_avg_ms": round(ring[0] / max(ring[1], 1), 5),
+                                  "band_avg_ms": round(band[0] / max(band[1], 1), 5),
                                   "interior_avg_ms": round(sweep[0] / max(sweep[1], 1), 5)}), flush=True)
     stencil.set_tuning(overlap=1)
-    os.environ.pop("SMI_ROUNDS_MULTI", None)
+    stencil.set_bands(0, 2)
     comm.finalize()
 
 
