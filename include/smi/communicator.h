@@ -22,7 +22,10 @@
  *     thread at a time (concurrent callers are serialised per transport
  *     group, but a second thread's operation would still interleave in the
  *     issue order and share the communicator's staging workspace).  The
- *     `port` argument of a bulk call is informational.
+ *     `port` argument of a bulk call is informational: bulk operations that
+ *     must run concurrently from different threads (the reference's
+ *     collectives on different ports) each take a communicator of their own
+ *     from smi_comm_dup.
  *   - element-granular channels (SMI_Push/SMI_Pop, SMI_Bcast, SMI_Reduce,
  *     SMI_Scatter, SMI_Gather) travel on a communicator of their own (an
  *     RCCL communicator split off at smi_init, pre-connected to every peer),
@@ -73,6 +76,17 @@ int smi_init(int rank, int size, int device, const void *unique_id, int id_bytes
  * to run multi-rank parity tests on a single GPU. */
 int smi_local_group_create(int size, int *group_id);
 int smi_init_local(int group_id, int rank, int device, SMI_Comm *comm);
+
+/* A new communicator over the same ranks, with its own matching spaces,
+ * comm stream and staging (MPI_Comm_dup; an RCCL communicator split off
+ * this one, or a new in-process group).  Collective: every rank calls it,
+ * in the same order relative to its other dups.  Bulk operations on
+ * different communicators are matched independently, so a communicator per
+ * port lets host threads drive bulk collectives on different ports at the
+ * same time -- what the reference's distinct ports give its concurrent
+ * collectives (microbenchmarks/kernels/multi_collectives.cl:50-76).
+ * Finalize every dup like any communicator. */
+int smi_comm_dup(SMI_Comm comm, SMI_Comm *out);
 
 int smi_finalize(SMI_Comm comm);
 

@@ -54,6 +54,7 @@ SIGNATURES = {
     "smi_local_group_create": (I, [I, ctypes.POINTER(I)]),
     "smi_init_local": (I, [I, I, I, ctypes.POINTER(SMI_Comm)]),
     "smi_finalize": (I, [SMI_Comm]),
+    "smi_comm_dup": (I, [SMI_Comm, ctypes.POINTER(SMI_Comm)]),
     "smi_device_count": (I, [ctypes.POINTER(I)]),
     "smi_stream_synchronize": (I, [P]),
     "smi_stencil_step": (I, [P, P, I, I, ctypes.POINTER(I), ctypes.POINTER(P), P, P, P]),

@@ -75,6 +75,31 @@ def _stale(variant: str = "") -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _deps(src: str, seen: set | None = None) -> set:
+    """src and every header it includes with "..." (recursively), resolved
+    against its directory, csrc/ and include/."""
+    import re
+    seen = set() if seen is None else seen
+    if src in seen or not os.path.exists(src):
+        return seen
+    seen.add(src)
+    with open(src, errors="replace") as f:
+        for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', f.read(), re.M):
+            for d in (os.path.dirname(src), CSRC, os.path.join(ROOT, "include")):
+                cand = os.path.join(d, inc)
+                if os.path.exists(cand):
+                    _deps(cand, seen)
+                    break
+    return seen
+
+
+def _obj_stale(src: str, obj: str, flags_file: str) -> bool:
+    if not os.path.exists(obj) or not os.path.exists(flags_file):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in _deps(src) | {flags_file})
+
+
 def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     lib = lib_path(variant)
     if not force and not _stale(variant):
@@ -83,15 +108,24 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     os.makedirs(out_dir, exist_ok=True)
     flags = CXXFLAGS + VARIANT_FLAGS[variant]
     hipcc = os.path.join(ROCM, "bin", "hipcc")
+    # objects are rebuilt when their source, a header they include or the
+    # flags changed (the flags are recorded next to the objects)
+    flags_file = os.path.join(out_dir, "flags.txt")
+    flags_txt = " ".join(flags + [f"{k}={v}" for k, v in sorted(FILE_FLAGS.items())])
+    if not os.path.exists(flags_file) or open(flags_file).read() != flags_txt:
+        with open(flags_file, "w") as f:
+            f.write(flags_txt)
     objs = []
     procs = []
     for src in sources():
         obj = os.path.join(out_dir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if not force and not _obj_stale(src, obj, flags_file):
+            continue
         cmd = [hipcc, *flags, *file_flags(src), "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
-        objs.append(obj)
     failed = []
     for src, p in procs:
         out, _ = p.communicate()

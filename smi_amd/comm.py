@@ -38,6 +38,14 @@ class Comm:
             raise _lib.SMIError("communicator finalized")
         return self._c
 
+    def dup(self) -> "Comm":
+        """smi_comm_dup: a communicator over the same ranks whose bulk
+        operations are matched independently of this one's (one per port for
+        concurrent bulk collectives from different threads).  Collective."""
+        c = _lib.SMI_Comm()
+        _lib.call("smi_comm_dup", self.handle, ctypes.byref(c))
+        return Comm(c, self.device)
+
     def finalize(self) -> None:
         if self._alive:
             _lib.call("smi_finalize", self._c)

@@ -14,7 +14,8 @@
 // reference's per-port channels.  Sends are detached through a ring of 32
 // staging slots -- the counterpart of the reference's credit window -- so a
 // rank may push before its peer pops.  Element reduce folds each element's
-// contributions with the same HIP fold kernel as smi_reduce.
+// contributions on the root with fold.h's fold_one, the same source as the
+// device fold kernel of smi_reduce.
 #include <algorithm>
 #include <cstring>
 #include <deque>
@@ -22,6 +23,7 @@
 #include <mutex>
 #include <unordered_map>
 
+#include "fold.h"
 #include "smi_internal.h"
 
 namespace smi {
@@ -46,10 +48,10 @@ struct Msg {
 
 struct ChanEngine {
     int device = 0;
-    hipStream_t send_stream = nullptr, recv_stream = nullptr, work_stream = nullptr;
+    hipStream_t send_stream = nullptr, recv_stream = nullptr;
     char *host_slots = nullptr, *dev_slots = nullptr;   // kSlots x kMsgBytes
     char *host_rslot = nullptr, *dev_rslot = nullptr;   // one receive message
-    char *host_red = nullptr, *dev_red = nullptr;       // element-reduce staging
+    std::vector<char> red_row;                          // element-reduce contributions (64 ranks x 8 B)
     SendTicket tickets[kSlots];
     int next_slot = 0;
     std::mutex send_mu, recv_mu, red_mu;
@@ -63,13 +65,10 @@ struct ChanEngine {
             if (t.ev) hipEventDestroy(t.ev);
         if (host_slots) hipHostFree(host_slots);
         if (host_rslot) hipHostFree(host_rslot);
-        if (host_red) hipHostFree(host_red);
         if (dev_slots) hipFree(dev_slots);
         if (dev_rslot) hipFree(dev_rslot);
-        if (dev_red) hipFree(dev_red);
         if (send_stream) hipStreamDestroy(send_stream);
         if (recv_stream) hipStreamDestroy(recv_stream);
-        if (work_stream) hipStreamDestroy(work_stream);
     }
 };
 
@@ -83,13 +82,11 @@ int get_engine(Comm *c, ChanEngine **out) {
         SMI_HIP_CHECK(hipSetDevice(c->device));
         SMI_HIP_CHECK(hipStreamCreateWithFlags(&e->send_stream, hipStreamNonBlocking));
         SMI_HIP_CHECK(hipStreamCreateWithFlags(&e->recv_stream, hipStreamNonBlocking));
-        SMI_HIP_CHECK(hipStreamCreateWithFlags(&e->work_stream, hipStreamNonBlocking));
         SMI_HIP_CHECK(hipHostMalloc(&e->host_slots, kSlots * kMsgBytes));
         SMI_HIP_CHECK(hipHostMalloc(&e->host_rslot, kMsgBytes));
-        SMI_HIP_CHECK(hipHostMalloc(&e->host_red, 2 * 64 * 8 + 64));
+        e->red_row.resize(64 * 8);
         SMI_HIP_CHECK(hipMalloc(&e->dev_slots, kSlots * kMsgBytes));
         SMI_HIP_CHECK(hipMalloc(&e->dev_rslot, kMsgBytes));
-        SMI_HIP_CHECK(hipMalloc(&e->dev_red, 2 * 64 * 8 + 64));
         c->chan_engine = e;
     }
     *out = static_cast<ChanEngine *>(c->chan_engine.get());
@@ -292,6 +289,32 @@ ChanState *begin_call(D *chan) {
 
 }  // namespace
 
+template <typename T, int S>
+int fold_element_t(const void *row, void *out, int n, int op) {
+    T v;
+    switch (op) {
+    case SMI_ADD: v = fold_one<T, S, SMI_ADD>((const T *)row, n); break;
+    case SMI_MAX: v = fold_one<T, S, SMI_MAX>((const T *)row, n); break;
+    case SMI_MIN: v = fold_one<T, S, SMI_MIN>((const T *)row, n); break;
+    default: set_error("unsupported reduce op"); return SMI_ERR_UNSUPPORTED;
+    }
+    memcpy(out, &v, sizeof(T));
+    return SMI_SUCCESS;
+}
+
+// one element of n contributions (row[k] = rank k's), SHIFT_REG per type
+// (codegen/ops.py:110-116)
+int fold_element(const void *row, void *out, int n, int type, int op) {
+    switch (type) {
+    case SMI_FLOAT: return fold_element_t<float, 4>(row, out, n, op);
+    case SMI_DOUBLE: return fold_element_t<double, 4>(row, out, n, op);
+    case SMI_INT: return fold_element_t<int32_t, 1>(row, out, n, op);
+    case SMI_SHORT: return fold_element_t<int16_t, 1>(row, out, n, op);
+    case SMI_CHAR: return fold_element_t<int8_t, 1>(row, out, n, op);
+    default: set_error("unsupported data type"); return SMI_ERR_UNSUPPORTED;
+    }
+}
+
 // The last packets of a channel are detached sends: their staging slots must
 // outlive them, so finalize waits until the peers have received them.
 int channels_drain(Comm *c) {
@@ -420,29 +443,19 @@ void SMI_Reduce(SMI_RChannel *chan, void *data_snd, void *data_rcv) {
         append(s, data_snd);
         if (s->fill == s->per_msg || last) rc = flush(s, root);
     } else {
-        // root: one element from every rank, folded in rank order on the GPU
-        // with the smi_reduce fold kernel (reduce.cl:65-69,100-105,120-125)
+        // root: the element of every rank in rank order (the packets the
+        // contributors streamed ahead are already unpacked host-side), folded
+        // by the support kernel's fold (fold.h, reduce.cl:65-69,100-105,
+        // 120-125) as they complete -- no device round trip per element (the
+        // previous per-element fold launch + sync ran at 47 k elements/s)
         ChanEngine *e = s->eng;
         std::lock_guard<std::mutex> lk(e->red_mu);
-        char *row = e->host_red;
+        char *row = e->red_row.data();
         for (int k = 0; k < n && rc == SMI_SUCCESS; ++k) {
             if (k == root) memcpy(row + (size_t)k * s->esz, data_snd, s->esz);
             else rc = take(s, k, row + (size_t)k * s->esz);
         }
-        if (rc == SMI_SUCCESS) {
-            char *dout = e->dev_red + 64 * 8;
-            if (hipSetDevice(s->comm->device) != hipSuccess ||
-                hipMemcpyAsync(e->dev_red, row, (size_t)n * s->esz, hipMemcpyHostToDevice, e->work_stream) != hipSuccess)
-                rc = SMI_ERR_HIP;
-            if (rc == SMI_SUCCESS)
-                rc = smi_reduce_fold(e->dev_red, dout, n, 1, 1, (SMI_Datatype)s->type, (SMI_Op)s->op, e->work_stream);
-            if (rc == SMI_SUCCESS &&
-                (hipMemcpyAsync(row + 64 * 8, dout, s->esz, hipMemcpyDeviceToHost, e->work_stream) != hipSuccess ||
-                 hipStreamSynchronize(e->work_stream) != hipSuccess))
-                rc = SMI_ERR_HIP;
-            if (rc == SMI_SUCCESS) memcpy(data_rcv, row + 64 * 8, s->esz);
-            else if (rc == SMI_ERR_HIP) set_error("SMI_Reduce: HIP call failed");
-        }
+        if (rc == SMI_SUCCESS) rc = fold_element(row, data_rcv, n, s->type, s->op);
     }
     chan->status = rc;
     if (last) close_chan(&chan->handle);

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "fold.h"
 #include "smi_internal.h"
 
 namespace smi {
@@ -29,40 +30,9 @@ struct FoldRows {
     const void *row[kMaxFoldRanks];
 };
 
-template <typename T, int OP>
-__device__ __forceinline__ T op_apply(T a, T b) {
-    if constexpr (OP == SMI_ADD) {
-        if constexpr (std::is_same<T, float>::value) return __fadd_rn(a, b);
-        else if constexpr (std::is_same<T, double>::value) return __dadd_rn(a, b);
-        else {
-            using U = typename std::make_unsigned<T>::type;  // wrapping add
-            return (T)(U)((U)a + (U)b);
-        }
-    } else if constexpr (OP == SMI_MAX) {
-        return a > b ? a : b;   // SMI_OP_MAX, include/smi/reduce_operations.h:6
-    } else {
-        return a < b ? a : b;   // SMI_OP_MIN, include/smi/reduce_operations.h:5
-    }
-}
-
-// codegen/ops.py:124-141 SHIFT_REG_INIT (note FLT_MIN / DBL_MIN, the
-// smallest positive normals, for MAX -- kept as the reference has it).
-template <typename T, int OP>
-__device__ __forceinline__ T op_init() {
-    if constexpr (OP == SMI_ADD) return (T)0;
-    else if constexpr (OP == SMI_MAX) {
-        if constexpr (std::is_same<T, float>::value) return 1.17549435e-38f;
-        else if constexpr (std::is_same<T, double>::value) return 2.2250738585072014e-308;
-        else return std::numeric_limits<T>::min();
-    } else {
-        if constexpr (std::is_same<T, float>::value) return 3.40282347e+38f;
-        else if constexpr (std::is_same<T, double>::value) return 1.7976931348623157e+308;
-        else return std::numeric_limits<T>::max();
-    }
-}
-
-// Fold of reduce.cl:65-69,100-105,120-125 for one element, contributions in
-// rank order, S slots (4 for float/double, 1 for the integer types).
+// Fold of reduce.cl:65-69,100-105,120-125 (fold.h's fold_one, vectorised):
+// contributions in rank order, S slots (4 for float/double, 1 for the
+// integer types).
 // Each thread folds E = VPT*VEC consecutive elements, loaded as VPT 16-byte
 // vectors per contribution row.  The rows are streamed exactly once, so the
 // default launch uses nontemporal loads/stores and one E-group per thread.

@@ -4,6 +4,7 @@
 // (codegen/templates/host_hlslib.cl:8-90): there are no routing tables to
 // load and no support kernels to fork -- rank r is GPU r, and the transport
 // is an RCCL communicator (or an in-process device-copy group for tests).
+#include <algorithm>
 #include <mutex>
 #include <unordered_map>
 
@@ -225,6 +226,25 @@ int smi_init_local(int group_id, int rank, int device, SMI_Comm *comm) {
     return finish_init(std::move(c), comm);
 }
 
+int smi_comm_dup(SMI_Comm comm, SMI_Comm *out) {
+    SMI_ARG_CHECK(out, "NULL output");
+    Comm *c = lookup_comm(comm);
+    if (!c) {
+        set_error("unknown communicator");
+        return SMI_ERR_BAD_COMM;
+    }
+    SMI_HIP_CHECK(hipSetDevice(c->device));
+    int rc = SMI_SUCCESS;
+    auto t = c->transport->dup(&rc);
+    if (rc != SMI_SUCCESS) return rc;
+    auto d = std::make_unique<Comm>();
+    d->rank = c->rank;
+    d->size = c->size;
+    d->device = c->device;
+    d->transport = std::move(t);
+    return finish_init(std::move(d), out);
+}
+
 int smi_finalize(SMI_Comm comm) {
     std::unique_ptr<Comm> c;
     {
@@ -295,18 +315,18 @@ int smi_prof_read_tag(int kernel, int tag, double *total_ms, long *launches, dou
 int smi_prof_list(int *kernels, int *tags, int max_entries, int *n_entries) {
     SMI_ARG_CHECK(n_entries && (max_entries == 0 || (kernels && tags)), "NULL output");
     std::lock_guard<std::mutex> lk(g_prof_mu);
-    int n = 0;
+    // distinct (kernel, tag) pairs in first-recorded order, independent of
+    // the caller's buffer (a max_entries = 0 size query counts them too)
+    std::vector<std::pair<int, int>> keys;
     for (auto &r : g_prof_recs) {
-        bool seen = false;
-        for (int i = 0; i < n && i < max_entries; ++i) seen |= kernels[i] == r.kernel && tags[i] == r.tag;
-        if (seen) continue;
-        if (n < max_entries) {
-            kernels[n] = r.kernel;
-            tags[n] = r.tag;
-        }
-        ++n;
+        const std::pair<int, int> k(r.kernel, r.tag);
+        if (std::find(keys.begin(), keys.end(), k) == keys.end()) keys.push_back(k);
     }
-    *n_entries = n;
+    for (int i = 0; i < (int)keys.size() && i < max_entries; ++i) {
+        kernels[i] = keys[i].first;
+        tags[i] = keys[i].second;
+    }
+    *n_entries = (int)keys.size();
     return SMI_SUCCESS;
 }
 

@@ -69,6 +69,10 @@ class Transport {
     // One receive, enqueued on `stream` (the caller synchronises).  Like
     // send_detached, safe to call from several host threads at once.
     virtual int recv_now(void *buf, size_t bytes, int peer, hipStream_t stream) = 0;
+    // A new transport over the same ranks with matching spaces of its own
+    // (smi_comm_dup).  Collective: every rank dups its transports in the same
+    // order.
+    virtual std::unique_ptr<Transport> dup(int *rc) = 0;
 };
 
 // One transport group, closed on every path: begin() takes the transport's
@@ -137,5 +141,9 @@ int prof_end(int token, hipStream_t stream);
 void prof_break_chain();
 
 size_t type_size(int type);
+
+// Device-to-device copies in one kernel launch (copy.hip); segments that are
+// not 16-byte aligned multiples go through hipMemcpyAsync.
+int launch_copies(const void *const *src, void *const *dst, const size_t *bytes, int n, hipStream_t s);
 
 }  // namespace smi

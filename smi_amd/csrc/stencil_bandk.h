@@ -19,7 +19,12 @@
 // to 80 us beside the interior, and took every slot the interior needed -- an
 // interior rank ran at 0.74-0.81 of a lone tile (profiles/r02/rehearsal/).
 // Here one wave walks a short run of rows down a column window, every input
-// row advancing K register-resident levels (the sweep's 3-slot rings):
+// row advancing K register-resident levels (the sweep's 3-slot rings).  Beside
+// the interior, which keeps HBM saturated, every load round trip takes
+// microseconds: a walk that loads its rows a batch ahead spent ~140 us per
+// pass in 16 dependent round trips (profiles/r03/).  So a wave first issues
+// LDS-DMA loads of ALL its input rows (1 KiB each, no VGPRs held) -- one
+// round trip -- and then walks them from LDS:
 //   top / bottom band: one 256-column window per wave (KC-column aprons),
 //     input rows [-K, 2K) -> output rows [0, K)   (3K rows walked)
 //   left / right band: four 64-column sub-windows per wave, each walking its
@@ -68,7 +73,24 @@ struct BandK {
     bool copyL, copyR, gT, gB;
     float4 W[K][3];   // level 0..K-1, slot = input row index mod 3
 
-    __device__ __forceinline__ float4 ld(int t) const { return *band_addr(a, K, rb + t, c); }
+    float4 *rows_lds;    // this wave's input rows in LDS: row t at rows_lds[t * 64 + lane]
+    unsigned rows_m0;    // their LDS byte address (wave-uniform)
+
+    __device__ __forceinline__ float4 ld(int t) const { return rows_lds[t * 64 + (threadIdx.x & 63)]; }
+
+    // LDS-DMA of input row t: lane i's 16 bytes (from wherever band_addr
+    // finds them: tile, halo or corner block) land at rows_m0 + 1024 t + 16 i
+    // (cdna_hip_programming.md, LDS-DMA recipe: M0 set and restored in the
+    // same statement)
+    __device__ __forceinline__ void dma(int t) const {
+        const float4 *src = band_addr(a, K, rb + t, c);
+        const unsigned dst = __builtin_amdgcn_readfirstlane(rows_m0 + 1024u * (unsigned)t);
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(dst)
+                     : "memory");
+    }
 
     // level step at row i with the global-edge copy rule per cell
     __device__ __forceinline__ float4 step(int i, const float4 &n, const float4 &m, const float4 &s) const {
@@ -124,6 +146,10 @@ struct BandK {
     }
 
     __device__ __forceinline__ void run(int n_in) {
+        // every input row in flight at once, one wait (hipcc does not count
+        // the asm loads: the wait is explicit)
+        for (int t = 0; t < n_in; ++t) dma(t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // prologue: input rows 0 .. 2K (n_in >= 3K > 2K), level l from input 2l on
         static_for<PRO>([&](auto T) {
             constexpr int t = T;
@@ -138,8 +164,8 @@ struct BandK {
             });
             if constexpr (t == 2 * K) store(t, v);
         });
-        // steady state: batches of 3 rows, loads one batch ahead (n_in is
-        // wave-uniform; loads past the end are clamped reads, never used)
+        // steady state: batches of 3 rows, LDS reads one batch ahead (n_in
+        // is wave-uniform; reads past the end hit spare rows, never used)
         float4 A[3], B[3];
 #pragma unroll
         for (int u = 0; u < 3; ++u) A[u] = ld(PRO + u);
@@ -159,16 +185,25 @@ struct BandK {
     }
 };
 
+// rows per wave: top/bottom 3K, left/right hb + 2K with hb <= 2K (launch_bandk
+// clamps it), + 6 spare rows for the reads one batch past the end
+template <int K>
+constexpr int bandk_lds_rows() { return 4 * K + 6; }
+
 template <int K>
 __global__ __launch_bounds__(64) void bandk_kernel(BandKArgs a) {
     using B = BandK<K>;
     constexpr int LL = B::LL;
+    __shared__ float4 rows_lds[bandk_lds_rows<K>() * 64];
     const int wv = blockIdx.x;
     const int band = (wv >= a.first[1]) + (wv >= a.first[2]) + (wv >= a.first[3]);
     const int lw = wv - (band == 0 ? 0 : band == 1 ? a.first[1] : band == 2 ? a.first[2] : a.first[3]);
     const int lane = threadIdx.x;
     const int X = a.rows, Y = a.cols;
     B w(a);
+    w.rows_lds = rows_lds;
+    w.rows_m0 = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) float4 *)(rows_lds));
     int o0, n_in;
     if (band < 2) {
         // top / bottom: window lw stores columns [lw sw, (lw + 1) sw)

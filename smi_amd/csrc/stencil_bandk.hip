@@ -1,6 +1,6 @@
 // stencil_bandk.hip -- host side of the halo-facing bands of a K-step pass
-// (kernel: stencil_bandk.h, one instantiation per K in stencilk_k<K>.hip),
-// the initial depth-K pack, and the rehearsal build's one-kernel exchange.
+// (kernel: stencil_bandk.h, one instantiation per K in stencilk_k<K>.hip)
+// and the initial depth-K pack.
 #include <cstdlib>
 
 #include "stencil_common.h"
@@ -19,9 +19,10 @@ SMI_BANDK_DECL(10)
 SMI_BANDK_DECL(11)
 SMI_BANDK_DECL(12)
 
-// Rows per left/right sub-window when not tuned: hb + 2K rows walked, so 2K
-// keeps a side wave's walk at 4K rows, close to a top/bottom wave's 3K.
-static int default_band_rows(int K) { return 2 * K; }
+// Rows per left/right sub-window when not tuned: hb + 2K rows walked; K keeps
+// a side wave's walk at 3K rows, a top/bottom wave's.  At most 2K (the
+// wave's LDS holds 4K rows).
+static int default_band_rows(int K) { return K; }
 
 int launch_bandk(int K, BandKArgs a, hipStream_t s) {
     const int X = a.rows, Y = a.cols;
@@ -33,7 +34,8 @@ int launch_bandk(int K, BandKArgs a, hipStream_t s) {
     const int nwin = (Y + a.sw - 1) / a.sw;
     a.rlo = a.has[0] ? K : 0;
     a.rhi = a.has[1] ? X - K : X;
-    a.hb = g_tune.band_rows > 0 ? g_tune.band_rows : default_band_rows(K);
+    // a side wave's rows (hb + 2K) must fit its LDS rows (4K + spares)
+    a.hb = std::min(g_tune.band_rows > 0 ? g_tune.band_rows : default_band_rows(K), 2 * K);
     a.nsub = a.rhi > a.rlo ? (a.rhi - a.rlo + a.hb - 1) / a.hb : 0;
     const int side_waves = (a.nsub + 3) / 4;
     const int waves_of[4] = {a.has[0] ? nwin : 0, a.has[1] ? nwin : 0, a.has[2] ? side_waves : 0,
@@ -94,33 +96,5 @@ int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hip
     return SMI_SUCCESS;
 }
 
-#ifdef SMI_LOOPBACK_REHEARSAL
-// Rehearsal build only: the 8-way loopback exchange as ONE copy kernel (an
-// RCCL send/recv group is one kernel launch too), so tools/rehearsal.py can
-// price the exchange without the in-process transport's per-message events.
-struct CopySegs {
-    const float4 *src[8];
-    float4 *dst[8];
-    int n4[8];
-};
-__global__ __launch_bounds__(256) void multicopy_kernel(CopySegs c, int nseg, int blocks_per_seg) {
-    const int seg = blockIdx.x / blocks_per_seg;
-    if (seg >= nseg) return;
-    const int b = blockIdx.x - seg * blocks_per_seg;
-    for (int i = b * 256 + threadIdx.x; i < c.n4[seg]; i += blocks_per_seg * 256) c.dst[seg][i] = c.src[seg][i];
-}
-int launch_multicopy(const float *const *src, float *const *dst, const size_t *bytes, int nseg, hipStream_t s) {
-    CopySegs c{};
-    for (int i = 0; i < nseg && i < 8; ++i) {
-        c.src[i] = reinterpret_cast<const float4 *>(src[i]);
-        c.dst[i] = reinterpret_cast<float4 *>(dst[i]);
-        c.n4[i] = (int)(bytes[i] / 16);
-    }
-    const int bps = 8;
-    hipLaunchKernelGGL(multicopy_kernel, dim3(bps * nseg), dim3(256), 0, s, c, nseg, bps);
-    SMI_HIP_CHECK(hipGetLastError());
-    return SMI_SUCCESS;
-}
-#endif
 
 }  // namespace smi

@@ -161,8 +161,5 @@ struct BandKArgs {
 };
 int launch_bandk(int K, BandKArgs a, hipStream_t s);
 int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s);
-#ifdef SMI_LOOPBACK_REHEARSAL
-int launch_multicopy(const float *const *src, float *const *dst, const size_t *bytes, int nseg, hipStream_t s);
-#endif
 
 }  // namespace smi

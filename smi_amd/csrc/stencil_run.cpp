@@ -128,11 +128,11 @@ static int exchangek(Comm *c, const Neighbours &nb, const float *tile, int rows,
 #ifdef SMI_LOOPBACK_REHEARSAL
     if (getenv("SMI_LOOPBACK_FUSED") && nb.top == 0 && nb.left == 0 && nb.tl == 0) {
         // rehearsal: the same 8 messages as one copy kernel (like one RCCL group)
-        const float *src[8] = {tile, tile + (size_t)(rows - K) * cols, h.send_left, h.send_right,
-                               h.send_corner[0], h.send_corner[1], h.send_corner[2], h.send_corner[3]};
-        float *dst[8] = {h.bot, h.top, h.right, h.left, h.corner[3], h.corner[2], h.corner[1], h.corner[0]};
+        const void *src[8] = {tile, tile + (size_t)(rows - K) * cols, h.send_left, h.send_right,
+                              h.send_corner[0], h.send_corner[1], h.send_corner[2], h.send_corner[3]};
+        void *dst[8] = {h.bot, h.top, h.right, h.left, h.corner[3], h.corner[2], h.corner[1], h.corner[0]};
         const size_t by[8] = {rb, rb, cb, cb, kb, kb, kb, kb};
-        return launch_multicopy(src, dst, by, 8, s);
+        return launch_copies(src, dst, by, 8, s);
     }
 #endif
     Group grp(tp);

@@ -80,10 +80,12 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
     int tok = -1;
-    // chained markers: within one smi_stencil_run (which restarts the chain)
-    // the sweeps on this stream follow each other with nothing but event
-    // waits in between (multi-rank: the wait for the previous pass's ring),
-    // so each pass is timed from the end of the previous one
+    // chained markers: within one smi_stencil_run (which restarts the
+    // chain) back-to-back single-tile sweeps are timed from the end of the
+    // previous one (one marker per pass).  The chain holds only while nothing
+    // else was recorded in between: in a multi-rank run with overlap the band
+    // kernel's markers on the comm stream break it, so each interior sweep
+    // gets its own begin marker and its time is its own duration.
     if (prof && prof_enabled())
         SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K,
                            true));

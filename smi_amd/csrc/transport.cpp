@@ -15,6 +15,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -31,7 +32,8 @@ class RcclTransport final : public Transport {
     // match a bulk receive of a collective or a stencil exchange -- the
     // reference's ports keep those streams apart the same way (one FIFO
     // per port).
-    RcclTransport(ncclComm_t c, ncclComm_t chan) : comm_(c), chan_(chan) {}
+    RcclTransport(ncclComm_t c, ncclComm_t chan, int rank, int size)
+        : comm_(c), chan_(chan), rank_(rank), size_(size) {}
     ~RcclTransport() override {
         if (chan_) ncclCommDestroy(chan_);
         if (comm_) ncclCommDestroy(comm_);
@@ -97,26 +99,65 @@ class RcclTransport final : public Transport {
     // connects point-to-point peers lazily inside ncclGroupEnd, with a
     // handshake both sides must join; doing it here, collectively, means no
     // later detached send depends on what its peer is doing.
+    // Collective: every peer blocks in this handshake until this rank joins
+    // it, so a local failure must not skip it.  If the device buffer or the
+    // stream cannot be had, the handshake still runs -- from pinned host
+    // memory / on the null stream -- and the error is returned after it, on
+    // this rank only; the peers complete their init and see the failure at
+    // their first operation with this rank instead of hanging here.
     int connect_all(int rank, int size) {
         if (size == 1) return SMI_SUCCESS;
-        char *d = nullptr;
+        char *d = nullptr, *h = nullptr;
         hipStream_t st = nullptr;
-        SMI_HIP_CHECK(hipMalloc(&d, 2 * (size_t)size));
-        int rc = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess ? SMI_SUCCESS : SMI_ERR_HIP;
-        if (rc == SMI_SUCCESS) rc = check(ncclGroupStart(), "ncclGroupStart");
+        int local = SMI_SUCCESS;
+        if (hipMalloc(&d, 2 * (size_t)size) != hipSuccess) {
+            d = nullptr;
+            local = SMI_ERR_HIP;
+            set_error("channel connect: hipMalloc failed");
+            if (hipHostMalloc(&h, 2 * (size_t)size, hipHostMallocMapped) != hipSuccess) h = nullptr;
+        }
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+            st = nullptr;  // the null stream carries the handshake instead
+            local = SMI_ERR_HIP;
+            set_error("channel connect: stream creation failed");
+        }
+        char *buf = d ? d : h;
+        int rc = buf ? check(ncclGroupStart(), "ncclGroupStart") : SMI_ERR_HIP;
         for (int p = 0; p < size && rc == SMI_SUCCESS; ++p) {
             if (p == rank) continue;
-            rc = check(ncclSend(d + p, 1, ncclUint8, p, chan_, st), "ncclSend");
-            if (rc == SMI_SUCCESS) rc = check(ncclRecv(d + size + p, 1, ncclUint8, p, chan_, st), "ncclRecv");
+            rc = check(ncclSend(buf + p, 1, ncclUint8, p, chan_, st), "ncclSend");
+            if (rc == SMI_SUCCESS) rc = check(ncclRecv(buf + size + p, 1, ncclUint8, p, chan_, st), "ncclRecv");
         }
-        if (rc == SMI_SUCCESS) rc = check(ncclGroupEnd(), "ncclGroupEnd");
+        if (buf && rc != SMI_ERR_HIP) {
+            const int e = check(ncclGroupEnd(), "ncclGroupEnd");  // close the group on every path
+            if (rc == SMI_SUCCESS) rc = e;
+        }
         if (rc == SMI_SUCCESS && hipStreamSynchronize(st) != hipSuccess) {
             set_error("channel connect: stream synchronize failed");
             rc = SMI_ERR_HIP;
         }
-        if (st) hipStreamDestroy(st);
-        hipFree(d);
-        return rc;
+        if (st) (void)hipStreamDestroy(st);
+        if (d) (void)hipFree(d);
+        if (h) (void)hipHostFree(h);
+        return rc != SMI_SUCCESS ? rc : local;
+    }
+
+    // Both communicators split again (color 0, same rank order): RCCL
+    // matches the new pair's operations separately from this pair's.
+    std::unique_ptr<Transport> dup(int *rc) override {
+        std::lock_guard<std::mutex> lk(bulk_mu_);
+        ncclComm_t c2 = nullptr, ch2 = nullptr;
+        *rc = check(ncclCommSplit(comm_, 0, rank_, &c2, nullptr), "ncclCommSplit");
+        if (*rc != SMI_SUCCESS) return nullptr;
+        *rc = check(ncclCommSplit(chan_, 0, rank_, &ch2, nullptr), "ncclCommSplit");
+        if (*rc != SMI_SUCCESS) {
+            ncclCommDestroy(c2);
+            return nullptr;
+        }
+        auto t = std::make_unique<RcclTransport>(c2, ch2, rank_, size_);
+        *rc = t->connect_all(rank_, size_);
+        if (*rc != SMI_SUCCESS) return nullptr;
+        return t;
     }
 
     static int check(ncclResult_t r, const char *what) {
@@ -127,6 +168,7 @@ class RcclTransport final : public Transport {
 
   private:
     ncclComm_t comm_ = nullptr, chan_ = nullptr;
+    int rank_ = 0, size_ = 1;
     hipStream_t stream_ = nullptr;
     std::mutex bulk_mu_, chan_mu_;
 };
@@ -149,7 +191,7 @@ std::unique_ptr<Transport> make_rccl_transport(int rank, int size,
         ncclCommDestroy(comm);
         return nullptr;
     }
-    auto t = std::make_unique<RcclTransport>(comm, chan);
+    auto t = std::make_unique<RcclTransport>(comm, chan, rank, size);
     *rc = t->connect_all(rank, size);
     if (*rc != SMI_SUCCESS) return nullptr;
     return t;
@@ -161,8 +203,8 @@ namespace {
 struct Post {
     const void *buf = nullptr;
     size_t bytes = 0;
-    hipEvent_t ready = nullptr;  // sender's stream reached the send
-    hipEvent_t done = nullptr;   // receiver's copy finished
+    hipEvent_t ready = nullptr;  // sender's stream reached the send (one per sender group)
+    hipEvent_t done = nullptr;   // receiver's copy finished (recorded by the receiver)
     bool copied = false;         // `done` has been recorded
     int status = SMI_SUCCESS;
 };
@@ -175,6 +217,7 @@ struct LocalGroup {
     // (send_detached / recv_now), matched FIFO within each space only
     std::map<std::tuple<int, int, int>, std::deque<std::shared_ptr<Post>>> mailbox;
     int joined = 0;
+    std::map<int, int> dups;  // k-th smi_comm_dup of this group -> its group id
 };
 
 std::mutex g_groups_mu;
@@ -223,12 +266,15 @@ class LocalTransport final : public Transport {
         return SMI_SUCCESS;
     }
 
-    // Rendezvous: (1) post every send with a `ready` event on our stream;
-    // (2) for every receive, wait for the matching post (FIFO per
-    // (src, dst) pair, like the reference's per-port FIFO order), make our
-    // stream wait on its `ready`, copy, record `done`; (3) make our stream
-    // wait for the `done` of each of our sends, so later work may reuse the
-    // send buffers.
+    // Rendezvous, with a constant number of host calls per group (an
+    // interior rank's K-step exchange is 8 sends + 8 receives per pass; one
+    // copy + two events per message cost more host time than the pass):
+    // (1) post every send, all sharing one `ready` event recorded on our
+    // stream; (2) take the matching post of every receive (FIFO per (src,
+    // dst) pair, like the reference's per-port FIFO order), make our stream
+    // wait on each distinct `ready`, copy them all with one kernel, record
+    // one `done`; (3) make our stream wait for the `done` of each receiver of
+    // our sends, so later work may reuse the send buffers.
     int end() override {
         const int rc = end_group();
         bulk_mu_.unlock();
@@ -236,27 +282,72 @@ class LocalTransport final : public Transport {
     }
     int end_group() {
         std::vector<std::shared_ptr<Post>> mine;
-        for (auto &s : sends_) {
+        hipEvent_t ready = nullptr;
+        if (!sends_.empty()) {
+            SMI_TRY(get_event(&ready));
+            SMI_HIP_CHECK(hipEventRecord(ready, stream_));
+        }
+        for (auto &sd : sends_) {
             auto p = std::make_shared<Post>();
-            p->buf = s.buf;
-            p->bytes = s.bytes;
-            SMI_HIP_CHECK(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
-            SMI_HIP_CHECK(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
-            SMI_HIP_CHECK(hipEventRecord(p->ready, stream_));
+            p->buf = sd.buf;
+            p->bytes = sd.bytes;
+            p->ready = ready;
             mine.push_back(p);
         }
-        {
-            std::lock_guard<std::mutex> lk(g_->mu);
-            for (size_t i = 0; i < sends_.size(); ++i)
-                g_->mailbox[{rank_, sends_[i].peer, 0}].push_back(mine[i]);
+        if (!mine.empty()) {
+            {
+                std::lock_guard<std::mutex> lk(g_->mu);
+                for (size_t i = 0; i < sends_.size(); ++i) g_->mailbox[{rank_, sends_[i].peer, 0}].push_back(mine[i]);
+            }
+            g_->cv.notify_all();
         }
-        g_->cv.notify_all();
 
         int rc = SMI_SUCCESS;
-        for (auto &r : recvs_) {
-            const int st = take(r.buf, r.bytes, r.peer, 0, stream_);
-            if (st != SMI_SUCCESS && rc == SMI_SUCCESS) rc = st;
+        if (!recvs_.empty()) {
+            std::vector<std::shared_ptr<Post>> got;
+            std::vector<const void *> src;
+            std::vector<void *> dst;
+            std::vector<size_t> by;
+            for (auto &r : recvs_) {
+                auto p = next_post(r.peer, 0);
+                if (p->bytes != r.bytes) {
+                    set_error("local transport: send/recv size mismatch");
+                    p->status = SMI_ERR_COMM;
+                    if (rc == SMI_SUCCESS) rc = SMI_ERR_COMM;
+                } else {
+                    src.push_back(p->buf);
+                    dst.push_back(r.buf);
+                    by.push_back(r.bytes);
+                }
+                got.push_back(p);
+            }
+            std::vector<hipEvent_t> waited;
+            int st = SMI_SUCCESS;
+            for (auto &p : got)
+                if (p->status == SMI_SUCCESS && std::find(waited.begin(), waited.end(), p->ready) == waited.end()) {
+                    waited.push_back(p->ready);
+                    if (hipStreamWaitEvent(stream_, p->ready, 0) != hipSuccess) st = SMI_ERR_HIP;
+                }
+            if (st == SMI_SUCCESS) st = launch_copies(src.data(), dst.data(), by.data(), (int)src.size(), stream_);
+            hipEvent_t done = nullptr;
+            if (get_event(&done) != SMI_SUCCESS || hipEventRecord(done, stream_) != hipSuccess) st = SMI_ERR_HIP;
+            if (st != SMI_SUCCESS) {
+                set_error("local transport: HIP copy failed");
+                if (rc == SMI_SUCCESS) rc = st;
+            }
+            {
+                std::lock_guard<std::mutex> lk(g_->mu);
+                for (auto &p : got) {
+                    p->done = done;
+                    if (p->status == SMI_SUCCESS) p->status = st;
+                    p->copied = true;
+                }
+            }
+            g_->cv.notify_all();
+            if (done) SMI_TRY(retire(done));
         }
+
+        std::vector<hipEvent_t> joined;
         for (auto &p : mine) {
             {
                 std::unique_lock<std::mutex> lk(g_->mu);
@@ -266,9 +357,12 @@ class LocalTransport final : public Transport {
                 set_error("local transport: peer failed to receive");
                 rc = p->status;
             }
-            SMI_HIP_CHECK(hipStreamWaitEvent(stream_, p->done, 0));
-            SMI_TRY(retire(p));
+            if (p->done && std::find(joined.begin(), joined.end(), p->done) == joined.end()) {
+                joined.push_back(p->done);
+                SMI_HIP_CHECK(hipStreamWaitEvent(stream_, p->done, 0));
+            }
         }
+        if (ready) SMI_TRY(retire(ready));
         sends_.clear();
         recvs_.clear();
         return rc;
@@ -283,8 +377,7 @@ class LocalTransport final : public Transport {
         auto p = std::make_shared<Post>();
         p->buf = buf;
         p->bytes = bytes;
-        SMI_HIP_CHECK(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
-        SMI_HIP_CHECK(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
+        SMI_TRY(get_event(&p->ready));
         SMI_HIP_CHECK(hipEventRecord(p->ready, stream));
         {
             std::lock_guard<std::mutex> lk(g_->mu);
@@ -300,7 +393,29 @@ class LocalTransport final : public Transport {
             set_error("recv: peer out of range");
             return SMI_ERR_INVALID_ARG;
         }
-        return take(buf, bytes, peer, 1, stream);
+        auto p = next_post(peer, 1);
+        int st = SMI_SUCCESS;
+        if (p->bytes != bytes) {
+            set_error("local transport: send/recv size mismatch");
+            st = SMI_ERR_COMM;
+        } else if (hipStreamWaitEvent(stream, p->ready, 0) != hipSuccess ||
+                   (bytes && hipMemcpyAsync(buf, p->buf, bytes, hipMemcpyDeviceToDevice, stream) != hipSuccess)) {
+            set_error("local transport: HIP copy failed");
+            st = SMI_ERR_HIP;
+        }
+        hipEvent_t done = nullptr;
+        if (get_event(&done) != SMI_SUCCESS || hipEventRecord(done, stream) != hipSuccess) {
+            if (st == SMI_SUCCESS) st = SMI_ERR_HIP;
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_->mu);
+            p->done = done;
+            p->status = st;
+            p->copied = true;
+        }
+        g_->cv.notify_all();
+        if (done) SMI_TRY(retire(done));
+        return st;
     }
     int ticket_wait(SendTicket *t) override {
         if (!t->live) return SMI_SUCCESS;
@@ -312,64 +427,60 @@ class LocalTransport final : public Transport {
         t->live = false;
         t->impl.reset();
         int st = p->status;
-        SMI_HIP_CHECK(hipEventSynchronize(p->done));
-        SMI_TRY(retire(p));
+        // `done` may since have been recycled and recorded again by the
+        // receiver: then this waits for that later work too (never less)
+        if (p->done) SMI_HIP_CHECK(hipEventSynchronize(p->done));
+        SMI_TRY(retire(p->ready));
         if (st != SMI_SUCCESS) set_error("local transport: peer failed to receive");
         return st;
     }
 
+    // The k-th dup of every rank of a group lands in one new group (created
+    // by whichever rank gets there first).
+    std::unique_ptr<Transport> dup(int *rc) override;
+
     ~LocalTransport() override {
         // finalize has synchronised the device: no queue references them now
         for (auto e : retired_) hipEventDestroy(e);
+        for (auto e : free_) hipEventDestroy(e);
     }
 
   private:
-    // A post's events may still be referenced by barrier packets that another
-    // rank's stream has not processed yet, so they are destroyed only after a
-    // device-wide synchronisation (at teardown, or when many have piled up).
-    int retire(const std::shared_ptr<Post> &p) {
+    // Event pool.  An event may still be referenced by barrier packets that
+    // another rank's stream has not processed yet, so a retired event is
+    // reused only after a device-wide synchronisation (when many have piled
+    // up); fresh ones are created only until the pool is warm.
+    int get_event(hipEvent_t *e) {
         std::lock_guard<std::mutex> lk(retire_mu_);
-        retired_.push_back(p->ready);
-        retired_.push_back(p->done);
-        if (retired_.size() >= 8192) {
+        if (!free_.empty()) {
+            *e = free_.back();
+            free_.pop_back();
+            return SMI_SUCCESS;
+        }
+        SMI_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        return SMI_SUCCESS;
+    }
+    int retire(hipEvent_t e) {
+        std::lock_guard<std::mutex> lk(retire_mu_);
+        retired_.push_back(e);
+        if (retired_.size() >= 4096) {
             SMI_HIP_CHECK(hipDeviceSynchronize());
-            for (auto e : retired_) SMI_HIP_CHECK(hipEventDestroy(e));
+            free_.insert(free_.end(), retired_.begin(), retired_.end());
             retired_.clear();
         }
         return SMI_SUCCESS;
     }
     std::mutex retire_mu_;
-    std::vector<hipEvent_t> retired_;
+    std::vector<hipEvent_t> retired_, free_;
 
-    // Wait for the next post from `peer` (FIFO per (src, dst), like the
-    // reference's per-port FIFO order), order `stream` after the sender's
-    // `ready` event, copy, and mark the post consumed.
-    int take(void *buf, size_t bytes, int peer, int space, hipStream_t stream) {
-        std::shared_ptr<Post> p;
-        {
-            std::unique_lock<std::mutex> lk(g_->mu);
-            auto &q = g_->mailbox[{peer, rank_, space}];
-            g_->cv.wait(lk, [&] { return !q.empty(); });
-            p = q.front();
-            q.pop_front();
-        }
-        int st = SMI_SUCCESS;
-        if (p->bytes != bytes) {
-            set_error("local transport: send/recv size mismatch");
-            st = SMI_ERR_COMM;
-        } else if (hipStreamWaitEvent(stream, p->ready, 0) != hipSuccess ||
-                   (bytes && hipMemcpyAsync(buf, p->buf, bytes, hipMemcpyDeviceToDevice, stream) != hipSuccess)) {
-            set_error("local transport: HIP copy failed");
-            st = SMI_ERR_HIP;
-        }
-        if (hipEventRecord(p->done, stream) != hipSuccess && st == SMI_SUCCESS) st = SMI_ERR_HIP;
-        {
-            std::lock_guard<std::mutex> lk(g_->mu);
-            p->status = st;
-            p->copied = true;
-        }
-        g_->cv.notify_all();
-        return st;
+    // the next post from `peer` in `space` (FIFO per (src, dst, space))
+    std::shared_ptr<Post> next_post(int peer, int space) {
+        std::unique_lock<std::mutex> lk(g_->mu);
+        auto &q = g_->mailbox[{peer, rank_, space}];
+        g_->cv.wait(lk, [&] { return !q.empty(); });
+        auto p = q.front();
+        q.pop_front();
+        return p;
     }
 
     struct Op {
@@ -379,10 +490,31 @@ class LocalTransport final : public Transport {
     };
     std::shared_ptr<LocalGroup> g_;
     int rank_;
+    int ndup_ = 0;
     std::mutex bulk_mu_;
     hipStream_t stream_ = nullptr;
     std::vector<Op> sends_, recvs_;
 };
+
+std::unique_ptr<Transport> LocalTransport::dup(int *rc) {
+    const int k = ++ndup_;
+    int id = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_->mu);
+        auto it = g_->dups.find(k);
+        if (it != g_->dups.end()) {
+            id = it->second;
+        } else {
+            auto ng = std::make_shared<LocalGroup>();
+            ng->size = g_->size;
+            std::lock_guard<std::mutex> lk2(g_groups_mu);
+            id = g_next_group++;
+            g_groups[id] = ng;
+            g_->dups[k] = id;
+        }
+    }
+    return make_local_transport(id, rank_, rc);
+}
 
 std::unique_ptr<Transport> make_local_transport(int group_id, int rank, int *rc) {
     auto g = find_group(group_id);

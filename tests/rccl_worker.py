@@ -191,6 +191,36 @@ def channel_cases(comm, rank, world, s):
         report(rank, "chan gather", got == [r * 1000 + i for r in range(world) for i in range(40)])
 
 
+def dup_cases(comm, rank, world, s):
+    """smi_comm_dup (an RCCL communicator split off this one): a reduce on the
+    communicator and a bcast on its dup, issued in OPPOSITE orders on even and
+    odd ranks, on two streams -- RCCL matches the two communicators apart."""
+    d = comm.dup()
+    s2 = torch.cuda.Stream()
+    count = 1 << 18
+    snd = torch.full((count,), rank + 1, dtype=torch.int32, device="cuda")
+    rcv = torch.zeros_like(snd)
+    buf = (torch.arange(count, dtype=torch.float32, device="cuda") if rank == 0
+           else torch.zeros(count, device="cuda"))
+    torch.cuda.synchronize()
+
+    def red():
+        collectives.reduce(comm, snd, rcv, "add", root=world - 1, stream=s)
+
+    def bc():
+        collectives.bcast(d, buf, root=0, stream=s2)
+
+    for f in ((red, bc) if rank % 2 == 0 else (bc, red)):
+        f()
+    s.synchronize()
+    s2.synchronize()
+    if rank == world - 1:
+        report(rank, "dup reduce", bool(torch.all(rcv == world * (world + 1) // 2)))
+    report(rank, "dup bcast", bool(torch.equal(buf, torch.arange(count, dtype=torch.float32, device="cuda"))))
+    dist.barrier()
+    d.finalize()
+
+
 def main():
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -201,7 +231,7 @@ def main():
     s = torch.cuda.Stream()
     try:
         with torch.cuda.stream(s):
-            for part in (bulk_cases, stencil_cases, channel_cases):
+            for part in (bulk_cases, stencil_cases, channel_cases, dup_cases):
                 part(comm, rank, world, s)
                 s.synchronize()
                 dist.barrier()

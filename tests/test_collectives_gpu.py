@@ -164,3 +164,55 @@ def test_bcast_pipelined_pieces(gpu, piece_bytes, pb, n):
     for root in (0, n - 1):
         for got in _group_bcast(n, data, root):
             assert np.array_equal(got, data)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_comm_dup_concurrent_ports(gpu, oracle_mod, n):
+    """smi_comm_dup: a communicator per port, each driven from its own host
+    thread (the reference's collectives on distinct ports,
+    microbenchmarks/kernels/multi_collectives.cl:50-76).  Every rank runs a
+    reduce chain on the communicator and a bcast chain on its dup at the same
+    time, the two threads of odd ranks starting in the opposite order; both
+    results stay exact."""
+    import threading
+    from smi_amd import LocalGroup, collectives
+
+    def fn(comm):
+        d = comm.dup()
+        out = {}
+        count = 1 << 16
+
+        def red():
+            s = torch.cuda.Stream()
+            snd = torch.full((count,), comm.rank + 1, dtype=torch.int32, device="cuda")
+            rcv = torch.empty_like(snd)
+            with torch.cuda.stream(s):
+                for _ in range(5):
+                    collectives.reduce(comm, snd, rcv, "add", root=0, stream=s)
+                s.synchronize()
+            out["reduce"] = rcv.cpu().numpy() if comm.rank == 0 else None
+
+        def bc():
+            s = torch.cuda.Stream()
+            buf = (torch.arange(count, dtype=torch.float32, device="cuda") if comm.rank == n - 1
+                   else torch.zeros(count, device="cuda"))
+            with torch.cuda.stream(s):
+                for _ in range(5):
+                    collectives.bcast(d, buf, root=n - 1, stream=s)
+                s.synchronize()
+            out["bcast"] = buf.cpu().numpy()
+
+        order = [red, bc] if comm.rank % 2 == 0 else [bc, red]
+        ts = [threading.Thread(target=f) for f in order]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        torch.cuda.synchronize()
+        d.finalize()
+        return out
+
+    res = LocalGroup(n).run(fn)
+    assert (res[0]["reduce"] == n * (n + 1) // 2).all()
+    for r in range(n):
+        assert np.array_equal(res[r]["bcast"], np.arange(1 << 16, dtype=np.float32)), r

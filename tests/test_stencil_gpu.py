@@ -482,3 +482,27 @@ def test_scaled_guard_fuzz(gpu, oracle_mod, seed):
         g[r0:r0 + h, c0:c0 + w] = (sgn * np.ldexp(rng.random(e.shape) + 0.5, e)).astype(np.float32)
     T = int(rng.integers(k, 3 * k + 2))
     assert np.array_equal(bits(_run_fused(g, T, k=k)), bits(oracle_mod.stencil(g, T))), (X, Y, k, T)
+
+
+def test_profiling_entries_distinct(gpu, oracle_mod):
+    """smi_prof_list counts distinct (kernel, tag) pairs, also for the
+    max_entries = 0 size query profiling.entries() starts with: a 41-step
+    run (passes of 11 + 10 + 10 + 10 steps) records four launches and lists
+    two pairs."""
+    import ctypes
+    from smi_amd import LocalGroup, _lib, profiling, stencil
+    comm = LocalGroup(1).comm(0)
+    t = torch.from_numpy(oracle_mod.init_uniform(256, 512, seed=3)).cuda()
+    profiling.reset()
+    profiling.enable(True)
+    stencil.run(comm, t, 3 * 12 + 5, 1, 1)
+    torch.cuda.synchronize()
+    profiling.enable(False)
+    n = ctypes.c_int()
+    _lib.call("smi_prof_list", None, None, 0, ctypes.byref(n))
+    ents = profiling.entries()
+    assert n.value == len(ents) == len(set(ents)), ents
+    assert sorted(ents) == [(profiling.SWEEPK, 10), (profiling.SWEEPK, 11)], ents
+    assert profiling.read_tag(profiling.SWEEPK, 10)[1] == 3
+    profiling.reset()
+    comm.finalize()

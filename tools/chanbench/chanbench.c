@@ -2,8 +2,9 @@
  * host of the reference drives it (one SMI_Push / SMI_Pop call per element,
  * examples/host + microbenchmarks/kernels/bandwidth_0.cl:13-35 shape), over
  * the in-process transport on one GPU: rank 0 pushes N elements to rank 1
- * (two host threads).  Also one SMI_Reduce element stream (3 ranks -> root)
- * and a SMI_Bcast stream.  Prints one JSON line per measurement.
+ * (two host threads).  Also SMI_Reduce element streams (4 ranks, int add;
+ * 8 ranks, fp32 add with the reference's n * i known answer) and a SMI_Bcast
+ * stream.  Prints one JSON line per measurement.
  *
  *   chanbench [N] */
 #include <pthread.h>
@@ -55,12 +56,20 @@ static void *rank_main(void *p) {
             SMI_Bcast(&c, &v);
             a->bad += v != (float)i;
         }
-    } else { /* element reduce to rank 0 */
+    } else if (a->mode == 2) { /* element reduce to rank 0 */
         SMI_RChannel c = SMI_Open_reduce_channel(g_n, SMI_INT, SMI_ADD, 2, 0, comm);
         for (int i = 0; i < g_n; ++i) {
             int s = i + a->rank, r = 0;
             SMI_Reduce(&c, &s, &r);
             if (a->rank == 0) a->bad += r != a->world * i + a->world * (a->world - 1) / 2;
+        }
+    } else { /* fp32 element reduce to the last rank: test/reduce/reduce.cl:17-20 KAT, n * i exact */
+        const int root = a->world - 1;
+        SMI_RChannel c = SMI_Open_reduce_channel(g_n, SMI_FLOAT, SMI_ADD, 3, root, comm);
+        for (int i = 0; i < g_n; ++i) {
+            float s = (float)(i & 0xffff), r = 0.f;
+            SMI_Reduce(&c, &s, &r);
+            if (a->rank == root) a->bad += r != (float)a->world * (float)(i & 0xffff);
         }
     }
     a->secs = now() - t0;
@@ -99,7 +108,7 @@ int main(int argc, char **argv) {
     run("SMI_Push/SMI_Pop int", 2, 0, 64);
     run("SMI_Push/SMI_Pop int", 2, 0, 1);
     run("SMI_Bcast float", 4, 1, 0);
-    g_n /= 20;  /* one fold kernel per element on the root */
     run("SMI_Reduce int add", 4, 2, 0);
+    run("SMI_Reduce float add", 8, 3, 0);
     return 0;
 }
