@@ -84,14 +84,16 @@ int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
 int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_flight);
 int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in_flight);
 
-/* Multi-rank K-step passes: band_rows = output rows per left/right band
- * sub-window of the band kernel (each walks band_rows + 2K rows; 0 =
- * automatic, 2K), interior_rounds = rounds of resident waves the interior
- * sweep is cut into (default 2: workgroups retire mid-pass, so the comm
- * stream's band kernel and RCCL kernels find slots).  Pass < 0 to keep.
- * Scheduling only: bit-identical results for every setting. */
-int smi_stencil_set_bands(int band_rows, int interior_rounds);
-int smi_stencil_get_bands(int *band_rows, int *interior_rounds);
+/* Multi-rank K-step passes: band_cus = CUs reserved for the band kernel and
+ * the halo exchange (0..128; 0 = they share the whole GPU with the interior
+ * sweep; > 0 = a CU-masked stream pair, the same number of CUs reserved on
+ * every XCD -- use multiples of 8 -- and the interior sweep in one round of
+ * waves on the other CUs); interior_rounds = rounds of resident waves the
+ * interior sweep is cut into when they share the GPU (workgroups retire
+ * mid-pass, so the band kernel and RCCL kernels find slots).  Pass < 0 to
+ * keep.  Scheduling only: bit-identical results for every setting. */
+int smi_stencil_set_bands(int band_cus, int interior_rounds);
+int smi_stencil_get_bands(int *band_cus, int *interior_rounds);
 
 /* One phase of a planned run: `passes` launches of `steps_per_pass` steps. */
 typedef struct {

@@ -1,6 +1,6 @@
 // stencil_bandk.h -- the halo-facing bands of a multi-rank K-step pass as
-// short register walks (instantiated per K beside sweepk_kernel<K> in
-// stencilk_k<K>.hip).
+// short register walks, one cell per lane (instantiated per K beside
+// sweepk_kernel<K> in stencilk_k<K>.hip).
 //
 // In a multi-rank run with K steps per pass, every tile cell within K rows of
 // a side with a neighbour, or within KC = 4 ceil(K/4) columns of one, depends
@@ -12,226 +12,237 @@
 // (stencil_smi.cl:183-224).  Per-cell arithmetic and the global-edge copy
 // rule are the sweep's (stencil_smi.cl:143-156), exact (x 0.25 every level).
 //
-// Shape.  The kernel runs beside the interior sweep on the comm stream, so
-// what it costs the interior is the wave slots it holds times how long it
-// holds them.  Round 2's ring kernel dealt the bands to 512 LDS workgroups
-// (2048 waves, K barrier-separated levels each): it took ~30 us alone and up
-// to 80 us beside the interior, and took every slot the interior needed -- an
-// interior rank ran at 0.74-0.81 of a lone tile (profiles/r02/rehearsal/).
-// Here one wave walks a short run of rows down a column window, every input
-// row advancing K register-resident levels (the sweep's 3-slot rings).  Beside
-// the interior, which keeps HBM saturated, every load round trip takes
-// microseconds: a walk that loads its rows a batch ahead spent ~140 us per
-// pass in 16 dependent round trips (profiles/r03/).  So a wave first issues
-// LDS-DMA loads of ALL its input rows (1 KiB each, no VGPRs held) -- one
-// round trip -- and then walks them from LDS:
-//   top / bottom band: one 256-column window per wave (KC-column aprons),
-//     input rows [-K, 2K) -> output rows [0, K)   (3K rows walked)
-//   left / right band: four 64-column sub-windows per wave, each walking its
-//     own block of hb rows (hb + 2K rows walked), storing the KC band columns
-//     (the DPP neighbour shifts run across the whole wave: a sub-window's edge
-//     lanes receive the next sub-window's values, and those lanes are apron)
-// About 200 waves of 60-odd rows each at 8192^2, K = 12.
+// Shape.  The band kernel sits on the critical path of every pass twice: the
+// exchange waits for it, and the next interior waits for it.  What bounds it
+// is the length of one wave's dependent walk, not bytes or total VALU work
+// (~5 MB and ~1 M wave-instructions at 8192^2, K = 12: a few us of the whole
+// GPU).  Round 2's LDS ring (barrier per level) took ~30 us alone; a float4
+// walk of 3K rows per wave with all rows staged in LDS took ~45 us alone
+// (54 KiB of LDS per wave: one wave per CU pair of SIMDs, ~9 k dependent
+// instructions each).  Here a lane owns ONE cell across the band, so a wave
+// is 64 cells wide and walks only the band's depth:
+//   top / bottom band: lanes = 64 columns, the wave walks rows [-K, 2K)
+//     (bottom: [X-2K, X+K)), level l evaluated where the output cone needs
+//     it (3K - 2l rows), the K output rows stored by lanes [K, 64-K)
+//   left / right band: transposed -- lanes = 64 rows, the wave walks the
+//     columns [-K, KC+K) (right: [Y-KC-K, Y+K)) of each lane's own row, N/S
+//     neighbours by DPP, the KC output columns stored by lanes [K, 64-K)
+// Every input of a wave is loaded up front into registers (one memory round
+// trip; beside the HBM-saturating interior sweep a round trip takes
+// microseconds, so a walk that waits on loads row by row is latency-bound),
+// then the walk runs fully unrolled from registers: ~276 cell-levels per lane
+// at K = 12, 4 VALU each (two of them DPP adds), ~800 waves of < 100 VGPRs.
 #pragma once
 
 #include "stencilk.h"
 
 namespace smi {
 
-// extended-tile address of the 4 cells (r, c..c+3), c a multiple of 4, r in
-// [-K, X+K), c in [-KC, Y+KC): tile, side halo, or corner block.  Rows /
-// columns beyond a global edge (no neighbour there) are clamped onto the
-// tile: those cells only ever feed cells the copy rule overrides.
-__device__ __forceinline__ const float4 *band_addr(const BandKArgs &a, int K, int r, int c) {
-    const int X = a.rows, Y = a.cols, KC = a.kc;
-    r = min(max(r, a.has[0] ? -K : 0), a.has[1] ? X + K - 1 : X - 1);
-    c = min(max(c, a.has[2] ? -KC : 0), a.has[3] ? Y + KC - 4 : Y - 4);
-    const bool rin = r >= 0 && r < X, cin = c >= 0 && c < Y;
-    const int rt = min(max(r, 0), X - 1), ct = min(max(c, 0), Y - 4);
-    const int hr = r < 0 ? r + K : r - X;  // halo row (valid when !rin)
-    const int hc = c < 0 ? c + KC : c - Y; // halo column (valid when !cin)
-    const float *tile = a.in + (size_t)rt * Y + ct;
-    const float *vert = (r < 0 ? a.h.top : a.h.bot) + (size_t)max(hr, 0) * Y + ct;
-    const float *horz = (c < 0 ? a.h.left : a.h.right) + (size_t)rt * KC + max(hc, 0);
-    const float *cb = r < 0 ? (c < 0 ? a.h.corner[0] : a.h.corner[1]) : (c < 0 ? a.h.corner[2] : a.h.corner[3]);
-    const float *corn = cb + max(hr, 0) * KC + max(hc, 0);
-    const float *p = (rin && cin) ? tile : rin ? horz : cin ? vert : corn;
-    return reinterpret_cast<const float4 *>(p);
+// Level step on one cell per lane, in the reference order
+// 0.25 * (((S + W) + E) + N).  ROWWALK: the wave walks down rows and its lanes
+// are columns (W / E from lanes -1 / +1, N the older and S the newer input);
+// else it walks along columns and its lanes are rows (N / S from lanes -1 /
+// +1, W older, E newer).  Lanes 0 / 63 get whatever the DPP leaves: they are
+// never stored and feed only lanes that are not either.
+template <bool ROWWALK>
+__device__ __forceinline__ float band_cell(float older, float c, float newer) {
+    if constexpr (ROWWALK)
+        return jacobi(newer, shr1_any(c), shl1_any(c), older);
+    else
+        return jacobi(shl1_any(c), older, newer, shr1_any(c));
 }
 
-template <int K>
-struct BandK {
-    static constexpr int LL = (K + 3) / 4;  // apron lanes per window side (4 LL = KC >= K columns)
-    static constexpr int PRO = 2 * K + 1;   // prologue rows (the last one stores the first output row)
+// Source of one extended-tile cell (r, c), r in [-K, X+K), c in [-KC, Y+KC):
+// tile, side halo ([row][KC]), top/bottom halo (K x Y) or corner block
+// (K x KC).  Rows / columns past a global edge (no neighbour there) are
+// clamped onto the tile: those cells only feed cells the copy rule overrides.
+// a wave-uniform value the optimiser cannot trace back to its memory slot
+template <typename T>
+__device__ __forceinline__ T val(T x) {
+    asm("" : "+s"(x));
+    return x;
+}
 
-    const BandKArgs &a;  // the kernel argument (a copy would live in scratch)
-    __device__ BandK(const BandKArgs &args) : a(args) {}
-    int rb;           // input row of t = 0 (this lane's sub-window: o0 - K)
-    int o1;           // end of this lane's output rows
-    int c;            // first column of this lane's 4 cells
-    bool st;          // this lane stores (band columns, live sub-window)
-    bool copyL, copyR, gT, gB;
-    float4 W[K][3];   // level 0..K-1, slot = input row index mod 3
-
-    float4 *rows_lds;    // this wave's input rows in LDS: row t at rows_lds[t * 64 + lane]
-    unsigned rows_m0;    // their LDS byte address (wave-uniform)
-
-    __device__ __forceinline__ float4 ld(int t) const { return rows_lds[t * 64 + (threadIdx.x & 63)]; }
-
-    // LDS-DMA of input row t: lane i's 16 bytes (from wherever band_addr
-    // finds them: tile, halo or corner block) land at rows_m0 + 1024 t + 16 i
-    // (cdna_hip_programming.md, LDS-DMA recipe: M0 set and restored in the
-    // same statement)
-    __device__ __forceinline__ void dma(int t) const {
-        const float4 *src = band_addr(a, K, rb + t, c);
-        const unsigned dst = __builtin_amdgcn_readfirstlane(rows_m0 + 1024u * (unsigned)t);
-        unsigned keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(src), "s"(dst)
-                     : "memory");
-    }
-
-    // level step at row i with the global-edge copy rule per cell
-    __device__ __forceinline__ float4 step(int i, const float4 &n, const float4 &m, const float4 &s) const {
-        const float w = shr1_any(m.w);
-        const float e = shl1_any(m.x);
-        float4 o;
-        o.x = jacobi(s.x, w, m.y, n.x);
-        o.y = jacobi(s.y, m.x, m.z, n.y);
-        o.z = jacobi(s.z, m.y, m.w, n.z);
-        o.w = jacobi(s.w, m.z, e, n.w);
-        const bool rcopy = (i == 0 && gT) || (i == a.rows - 1 && gB);
-        o.x = (rcopy || copyL) ? m.x : o.x;
-        o.y = rcopy ? m.y : o.y;
-        o.z = rcopy ? m.z : o.z;
-        o.w = (rcopy || copyR) ? m.w : o.w;
-        return o;
-    }
-
-    // level l at input t from the level l-1 rows of inputs t-2 (N), t-1, t (S)
-    template <int PH>
-    __device__ __forceinline__ float4 level(int l, int t, const float4 (&P)[3]) const {
-        return step(rb + t - l, P[(PH + 1) % 3], P[(PH + 2) % 3], P[PH]);
-    }
-
-    __device__ __forceinline__ void store(int t, const float4 &v) const {
-        const int j = rb + K + (t - 2 * K);  // output row o0 + t - 2K
-        if (!st || j >= o1) return;
-        const int X = a.rows, Y = a.cols, KC = a.kc;
-        *reinterpret_cast<float4 *>(a.out + (size_t)j * Y + c) = v;
-        if (!a.pack) return;
-        // tee the next exchange's sends: columns [0, KC) / [Y-KC, Y) packed
-        // [row][KC], and the K x KC corner blocks
-        const bool L = c < KC, R = c >= Y - KC;
-        const int q = L ? c : c - (Y - KC);
-        if (L || R) {
-            *reinterpret_cast<float4 *>((L ? a.h.send_left : a.h.send_right) + (size_t)j * KC + q) = v;
-            if (j < K) *reinterpret_cast<float4 *>((L ? a.h.send_corner[0] : a.h.send_corner[1]) + j * KC + q) = v;
-            if (j >= X - K)
-                *reinterpret_cast<float4 *>((L ? a.h.send_corner[2] : a.h.send_corner[3]) + (j - (X - K)) * KC + q) = v;
-        }
-    }
-
-    template <int PH>
-    __device__ __forceinline__ void advance(int t, const float4 &x) {
-        W[0][PH] = x;
-        float4 v;
-        static_for<K>([&](auto L) {
-            constexpr int l = L + 1;
-            v = level<PH>(l, t, W[l - 1]);
-            if constexpr (l < K) W[l][PH] = v;
-        });
-        store(t, v);
-    }
-
-    __device__ __forceinline__ void run(int n_in) {
-        // every input row in flight at once, one wait (hipcc does not count
-        // the asm loads: the wait is explicit)
-        for (int t = 0; t < n_in; ++t) dma(t);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // prologue: input rows 0 .. 2K (n_in >= 3K > 2K), level l from input 2l on
-        static_for<PRO>([&](auto T) {
-            constexpr int t = T;
-            W[0][t % 3] = ld(t);
-            float4 v;
-            static_for<K>([&](auto L) {
-                constexpr int l = L + 1;
-                if constexpr (t >= 2 * l) {
-                    v = level<t % 3>(l, t, W[l - 1]);
-                    if constexpr (l < K) W[l][t % 3] = v;
-                }
-            });
-            if constexpr (t == 2 * K) store(t, v);
-        });
-        // steady state: batches of 3 rows, LDS reads one batch ahead (n_in
-        // is wave-uniform; reads past the end hit spare rows, never used)
-        float4 A[3], B[3];
-#pragma unroll
-        for (int u = 0; u < 3; ++u) A[u] = ld(PRO + u);
-        for (int t = PRO; t < n_in; t += 6) {
-#pragma unroll
-            for (int u = 0; u < 3; ++u) B[u] = ld(t + 3 + u);
-            static_for<3>([&](auto V) {
-                if (t + V < n_in) advance<(PRO + V) % 3>(t + V, A[V]);
-            });
-            if (t + 3 >= n_in) break;
-#pragma unroll
-            for (int u = 0; u < 3; ++u) A[u] = ld(t + 6 + u);
-            static_for<3>([&](auto V) {
-                if (t + 3 + V < n_in) advance<(PRO + 3 + V) % 3>(t + 3 + V, B[V]);
-            });
-        }
+struct BandSrc {
+    const float *in, *top, *bot, *left, *right, *c0, *c1, *c2, *c3;
+    int X, Y, KC, K;
+    bool hT, hB, hL, hR;
+    __device__ __forceinline__ BandSrc(const BandKArgs &a, int K_)
+        : in(a.in), top(a.h.top), bot(a.h.bot), left(a.h.left), right(a.h.right), c0(a.h.corner[0]),
+          c1(a.h.corner[1]), c2(a.h.corner[2]), c3(a.h.corner[3]), X(a.rows), Y(a.cols), KC(a.kc), K(K_),
+          hT(a.has[0]), hB(a.has[1]), hL(a.has[2]), hR(a.has[3]) {}
+    __device__ __forceinline__ const float *at(int r, int c) const {
+        r = min(max(r, hT ? -K : 0), hB ? X + K - 1 : X - 1);
+        c = min(max(c, hL ? -KC : 0), hR ? Y + KC - 1 : Y - 1);
+        const bool rin = r >= 0 && r < X, cin = c >= 0 && c < Y;
+        const int rt = min(max(r, 0), X - 1), ct = min(max(c, 0), Y - 1);
+        const int hr = r < 0 ? r + K : r - X;   // halo row (valid when !rin)
+        const int hc = c < 0 ? c + KC : c - Y;  // halo column (valid when !cin)
+        // (base, row index, row stride, column index) of the region
+        // (selects between opaque values: a select between two fields would
+        // be folded into a load from a computed address inside the struct,
+        // which keeps it in scratch)
+        const float *side = c < 0 ? val(left) : val(right);
+        const float *vert = r < 0 ? val(top) : val(bot);
+        const float *corn = r < 0 ? (c < 0 ? val(c0) : val(c1)) : (c < 0 ? val(c2) : val(c3));
+        const float *base = rin ? (cin ? val(in) : side) : (cin ? vert : corn);
+        const int ri = rin ? rt : hr, ci = cin ? ct : hc, stride = cin ? Y : KC;
+        return base + (size_t)ri * stride + ci;
     }
 };
 
-// rows per wave: top/bottom 3K, left/right hb + 2K with hb <= 2K (launch_bandk
-// clamps it), + 6 spare rows for the reads one batch past the end
 template <int K>
-constexpr int bandk_lds_rows() { return 4 * K + 6; }
+struct BandW {
+    static constexpr int KC = kc_of(K);
+    static constexpr int SW = 64 - 2 * K;  // stored lanes (cells) per wave
+    static constexpr int NR = 3 * K;       // inputs of a row walk
+    static constexpr int NC = 2 * K + KC;  // inputs of a column walk
+    static constexpr int G4 = 3 * KC / 4;  // float4 groups a column-walk lane loads
 
-template <int K>
-__global__ __launch_bounds__(64) void bandk_kernel(BandKArgs a) {
-    using B = BandK<K>;
-    constexpr int LL = B::LL;
-    __shared__ float4 rows_lds[bandk_lds_rows<K>() * 64];
-    const int wv = blockIdx.x;
-    const int band = (wv >= a.first[1]) + (wv >= a.first[2]) + (wv >= a.first[3]);
-    const int lw = wv - (band == 0 ? 0 : band == 1 ? a.first[1] : band == 2 ? a.first[2] : a.first[3]);
-    const int lane = threadIdx.x;
-    const int X = a.rows, Y = a.cols;
-    B w(a);
-    w.rows_lds = rows_lds;
-    w.rows_m0 = __builtin_amdgcn_readfirstlane(
-        (unsigned)(uintptr_t)(__attribute__((address_space(3))) float4 *)(rows_lds));
-    int o0, n_in;
-    if (band < 2) {
-        // top / bottom: window lw stores columns [lw sw, (lw + 1) sw)
-        w.c = lw * a.sw - 4 * LL + 4 * lane;
-        o0 = band == 0 ? 0 : X - K;
-        w.o1 = o0 + K;
-        n_in = 3 * K;
-        w.st = lane >= LL && lane < 64 - LL && w.c < Y;
-    } else {
-        // left / right: sub-window (lw, lane / 16) of 16 lanes, hb rows
-        const int li = lane & 15, sub = lw * 4 + (lane >> 4);
-        w.c = (band == 2 ? -4 * LL : Y + 4 * LL - 64) + 4 * li;
-        o0 = a.rlo + sub * a.hb;
-        w.o1 = min(o0 + a.hb, a.rhi);
-        n_in = a.hb + 2 * K;
-        w.st = li >= LL && li < 16 - LL && sub < a.nsub && (band == 2 ? w.c < a.kc : w.c >= Y - a.kc);
+    // The walk over N register-resident inputs: level l at input t (t >= 2l)
+    // is the cell at walk position t - l, from level l-1 at inputs t-2,
+    // t-1, t (3-slot ring per level, slot = t mod 3, compile-time).  The
+    // level-K value of input t (t >= 2K) goes to out(t - 2K, v).  CP: this
+    // lane copies its cell every step (global edge across the walk).
+    template <bool ROWWALK, bool CP, int N, typename Out>
+    __device__ __forceinline__ static void walk(const float (&x)[N], bool cp, Out &&out) {
+        float W[K][3];
+        static_for<N>([&](auto T) {
+            constexpr int t = T;
+            W[0][t % 3] = x[t];
+            float v = 0.0f;
+            static_for<K>([&](auto L) {
+                constexpr int l = L + 1;
+                if constexpr (t >= 2 * l) {
+                    const float c = W[l - 1][(t + 2) % 3];
+                    v = band_cell<ROWWALK>(W[l - 1][(t + 1) % 3], c, W[l - 1][t % 3]);
+                    if constexpr (CP) v = cp ? c : v;
+                    if constexpr (l < K) W[l][t % 3] = v;
+                }
+            });
+            if constexpr (t >= 2 * K) out(std::integral_constant<int, t - 2 * K>{}, v);
+        });
     }
-    w.rb = o0 - K;
-    w.gT = !a.has[0];
-    w.gB = !a.has[1];
-    w.copyL = !a.has[2] && w.c == 0;
-    w.copyR = !a.has[3] && w.c + 4 == Y;
-    w.run(n_in);
+
+    // top (BOT = false) or bottom band: lane = column c, rows r0 + t
+    template <bool BOT, bool CP>
+    __device__ __forceinline__ static void rows(const BandKArgs &a, int w, int lane) {
+        const int X = a.rows, Y = a.cols;
+        const int c = w * SW - K + lane;
+        const int r0 = BOT ? X - 2 * K : -K;
+        // the lane's sources: halo rows (top: inputs [0, K); bottom: [2K, 3K))
+        // from one base with one stride, tile rows from another
+        const int th = BOT ? 2 * K : 0;  // first halo input
+        const int tt = BOT ? 0 : K;      // first tile input
+        const BandSrc src(a, K);
+        const float *ph = src.at(r0 + th, c);
+        const float *pt = src.at(r0 + tt, c);
+        const int sh = (int)(src.at(r0 + th + 1, c) - ph);
+        const int st = (int)(src.at(r0 + tt + 1, c) - pt);
+        float x[NR];
+        static_for<NR>([&](auto T) {
+            constexpr int t = T;
+            constexpr bool halo = BOT ? t >= 2 * K : t < K;
+            x[t] = halo ? ph[(t - th) * sh] : pt[(t - tt) * st];
+        });
+        const bool store = lane >= K && lane < 64 - K && c < Y;
+        const bool cp = (!a.has[2] && c == 0) || (!a.has[3] && c == Y - 1);
+        const int KCr = a.kc;
+        walk<true, CP>(x, cp, [&](auto Q, float v) {
+            constexpr int q = Q;  // output row r0 + K + q
+            if (!store) return;
+            const int r = r0 + K + q;
+            a.out[(size_t)r * Y + c] = v;
+            if (!a.pack) return;
+            // tee: packed side columns and this band's two K x KC corner blocks
+            if (c < KCr) {
+                a.h.send_left[(size_t)r * KCr + c] = v;
+                a.h.send_corner[BOT ? 2 : 0][q * KCr + c] = v;
+            }
+            if (c >= Y - KCr) {
+                a.h.send_right[(size_t)r * KCr + c - (Y - KCr)] = v;
+                a.h.send_corner[BOT ? 3 : 1][q * KCr + c - (Y - KCr)] = v;
+            }
+        });
+    }
+
+    // left (RIGHT = false) or right band: lane = row r, columns c0 + t
+    template <bool RIGHT, bool CP>
+    __device__ __forceinline__ static void cols(const BandKArgs &a, int w, int lane) {
+        const int X = a.rows, Y = a.cols;
+        const int r = a.rlo + w * SW - K + lane;
+        // float4 groups [-KC, 2KC) (right: [Y - 2KC, Y + KC)); the walk starts
+        // KC - K columns in, at column -K (right: Y - KC - K)
+        const int g0 = RIGHT ? Y - 2 * KC : -KC;
+        const BandSrc src(a, K);
+        float4 g[G4];
+        static_for<G4>([&](auto G) {
+            constexpr int j = G;
+            g[j] = *reinterpret_cast<const float4 *>(src.at(r, g0 + 4 * j));
+        });
+        float x[NC];
+        static_for<NC>([&](auto T) {
+            constexpr int e = (KC - K) + T;
+            const float4 &q = g[e / 4];
+            x[T] = e % 4 == 0 ? q.x : e % 4 == 1 ? q.y : e % 4 == 2 ? q.z : q.w;
+        });
+        const bool store = lane >= K && lane < 64 - K && r < a.rhi;
+        const bool cp = (!a.has[0] && r == 0) || (!a.has[1] && r == X - 1);
+        float o[KC];
+        walk<false, CP>(x, cp, [&](auto Q, float v) { o[Q] = v; });
+        if (!store) return;
+        const int c0 = RIGHT ? Y - KC : 0;
+        float *send = RIGHT ? a.h.send_right : a.h.send_left;
+        static_for<KC / 4>([&](auto G) {
+            constexpr int j = 4 * G;
+            const float4 v = make_float4(o[j], o[j + 1], o[j + 2], o[j + 3]);
+            *reinterpret_cast<float4 *>(a.out + (size_t)r * Y + c0 + j) = v;
+            if (a.pack) {
+                *reinterpret_cast<float4 *>(send + (size_t)r * KC + j) = v;
+                // corner blocks of rows this band owns (only when the top /
+                // bottom side is a global edge, i.e. never sent)
+                if (r < K) *reinterpret_cast<float4 *>(a.h.send_corner[RIGHT ? 1 : 0] + r * KC + j) = v;
+                if (r >= X - K)
+                    *reinterpret_cast<float4 *>(a.h.send_corner[RIGHT ? 3 : 2] + (r - (X - K)) * KC + j) = v;
+            }
+        });
+    }
+};
+
+// one wave per 64-cell run of a band: waves [first[0], first[1]) top,
+// [first[1], first[2]) bottom, [first[2], first[3]) left, [first[3],
+// first[4]) right; four independent waves per workgroup
+template <int K>
+__global__ __launch_bounds__(256) void bandk_kernel(BandKArgs a) {
+    using B = BandW<K>;
+    const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+    if (wv >= a.first[4]) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int band = (wv >= a.first[1]) + (wv >= a.first[2]) + (wv >= a.first[3]);
+    // (no dynamic index into the kernel argument: that would copy it to scratch)
+    const int w = wv - (band == 0 ? 0 : band == 1 ? a.first[1] : band == 2 ? a.first[2] : a.first[3]);
+    const int X = a.rows, Y = a.cols;
+    if (band < 2) {
+        // does this wave hold column 0 or Y-1 of a global left / right edge?
+        const int c_lo = w * B::SW - K, c_hi = c_lo + 63;
+        const bool cp = (!a.has[2] && c_lo <= 0 && c_hi >= 0) || (!a.has[3] && c_lo <= Y - 1 && c_hi >= Y - 1);
+        if (band == 0)
+            cp ? B::template rows<false, true>(a, w, lane) : B::template rows<false, false>(a, w, lane);
+        else
+            cp ? B::template rows<true, true>(a, w, lane) : B::template rows<true, false>(a, w, lane);
+    } else {
+        const int r_lo = a.rlo + w * B::SW - K, r_hi = r_lo + 63;
+        const bool cp = (!a.has[0] && r_lo <= 0 && r_hi >= 0) || (!a.has[1] && r_lo <= X - 1 && r_hi >= X - 1);
+        if (band == 2)
+            cp ? B::template cols<false, true>(a, w, lane) : B::template cols<false, false>(a, w, lane);
+        else
+            cp ? B::template cols<true, true>(a, w, lane) : B::template cols<true, false>(a, w, lane);
+    }
 }
 
 template <int K>
 int bandk_launch_impl(const BandKArgs &a, int waves, hipStream_t s) {
-    hipLaunchKernelGGL((bandk_kernel<K>), dim3(waves), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((bandk_kernel<K>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
     SMI_HIP_CHECK(hipGetLastError());
     return SMI_SUCCESS;
 }

@@ -19,27 +19,18 @@ SMI_BANDK_DECL(10)
 SMI_BANDK_DECL(11)
 SMI_BANDK_DECL(12)
 
-// Rows per left/right sub-window when not tuned: hb + 2K rows walked; K keeps
-// a side wave's walk at 3K rows, a top/bottom wave's.  At most 2K (the
-// wave's LDS holds 4K rows).
-static int default_band_rows(int K) { return K; }
-
 int launch_bandk(int K, BandKArgs a, hipStream_t s) {
     const int X = a.rows, Y = a.cols;
-    const int LL = (K + 3) / 4;
     a.kc = kc_of(K);
     SMI_ARG_CHECK(K >= SWEEPK_MIN && K <= SWEEPK_MAX, "bandk: K must be 3..12");
     SMI_ARG_CHECK(X >= 2 * K && Y >= 2 * a.kc && Y % 4 == 0, "bandk: tile smaller than 2K x 2KC");
-    a.sw = 256 - 8 * LL;
-    const int nwin = (Y + a.sw - 1) / a.sw;
+    // one wave per 64 - 2K cells along a band (stencil_bandk.h)
+    a.sw = 64 - 2 * K;
     a.rlo = a.has[0] ? K : 0;
     a.rhi = a.has[1] ? X - K : X;
-    // a side wave's rows (hb + 2K) must fit its LDS rows (4K + spares)
-    a.hb = std::min(g_tune.band_rows > 0 ? g_tune.band_rows : default_band_rows(K), 2 * K);
-    a.nsub = a.rhi > a.rlo ? (a.rhi - a.rlo + a.hb - 1) / a.hb : 0;
-    const int side_waves = (a.nsub + 3) / 4;
-    const int waves_of[4] = {a.has[0] ? nwin : 0, a.has[1] ? nwin : 0, a.has[2] ? side_waves : 0,
-                             a.has[3] ? side_waves : 0};
+    const int nrow = (Y + a.sw - 1) / a.sw;
+    const int ncol = a.rhi > a.rlo ? (a.rhi - a.rlo + a.sw - 1) / a.sw : 0;
+    const int waves_of[4] = {a.has[0] ? nrow : 0, a.has[1] ? nrow : 0, a.has[2] ? ncol : 0, a.has[3] ? ncol : 0};
     int n = 0;
     for (int k = 0; k < 4; ++k) {
         a.first[k] = n;

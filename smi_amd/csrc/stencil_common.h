@@ -76,7 +76,10 @@ struct Tuning {
     // where workgroups retire, so the RCCL kernel of the exchange is never
     // left without a slot until the interior ends.
     int rounds_multi = 2;
-    int band_rows = 0;  // rows per left/right band sub-window (stencil_bandk.h); 0 = automatic
+    // CUs reserved for the band kernel and the exchange of multi-rank runs
+    // (0: they share the whole GPU with the interior sweep; > 0: CU-masked
+    // stream pair, the interior in one round of waves on the other CUs)
+    int band_cus = 0;
     int uk = 3;        // rows loaded ahead (K-step sweep: one 3-row register batch, fixed at build time)
 };
 extern Tuning g_tune;
@@ -128,6 +131,7 @@ __host__ __device__ constexpr int sweepk_apron_lanes(int K) { return K >= 9 ? 4 
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s);
 int launch_sweepk_ex(int K, const SweepKArgs &a, int ht, int reserve, bool prof, hipStream_t s);
 int sweepk_window_cols(int K);  // output columns per 256-column window
+int resident_waves_of(int K);   // waves of sweepk<K> one round of the whole GPU holds
 
 // Depth-K halos (stencil_bandk.h / stencil_bandk.hip).  KC = 4 ceil(K/4):
 // the column depth, whole float4 groups.  Receive side: top = rows -K..-1 and
@@ -154,10 +158,8 @@ struct BandKArgs {
     HaloK h;
     // filled by launch_bandk
     int first[5];      // first wave of band top, bottom, left, right; first[4] = all waves
-    int sw;            // output columns per top/bottom window
+    int sw;            // cells stored per wave (64 - 2K)
     int rlo, rhi;      // rows of the left/right bands
-    int hb;            // output rows per left/right sub-window
-    int nsub;          // sub-windows per left/right band
 };
 int launch_bandk(int K, BandKArgs a, hipStream_t s);
 int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s);

@@ -275,15 +275,15 @@ int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in
     return SMI_SUCCESS;
 }
 
-int smi_stencil_set_bands(int band_rows, int interior_rounds) {
-    SMI_ARG_CHECK(band_rows <= 65536 && interior_rounds <= 64, "band_rows / interior_rounds out of range");
-    if (band_rows >= 0) g_tune.band_rows = band_rows;
+int smi_stencil_set_bands(int band_cus, int interior_rounds) {
+    SMI_ARG_CHECK(band_cus <= 128 && interior_rounds <= 64, "band_cus / interior_rounds out of range");
+    if (band_cus >= 0) g_tune.band_cus = band_cus;
     if (interior_rounds >= 0) g_tune.rounds_multi = std::max(1, interior_rounds);
     return SMI_SUCCESS;
 }
 
-int smi_stencil_get_bands(int *band_rows, int *interior_rounds) {
-    if (band_rows) *band_rows = g_tune.band_rows;
+int smi_stencil_get_bands(int *band_cus, int *interior_rounds) {
+    if (band_cus) *band_cus = g_tune.band_cus;
     if (interior_rounds) *interior_rounds = g_tune.rounds_multi;
     return SMI_SUCCESS;
 }
@@ -322,7 +322,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     SMI_ARG_CHECK(px >= 1 && py >= 1 && px * py == c->size, "px*py must equal the communicator size");
     SMI_ARG_CHECK(timesteps >= 0, "timesteps < 0");
     SMI_ARG_CHECK(result_index, "NULL result_index");
-    hipStream_t s = (hipStream_t)stream_;
+    hipStream_t s = (hipStream_t)stream_;  // main stream: the caller's, or the CU-masked one
     hipStream_t cs = c->comm_stream;
     const int rows = x_local, cols = y_local;
     Neighbours nb = neighbours_of(c->rank, px, py);
@@ -479,6 +479,19 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     // the first phase the reference's artificial timestep t=0,
     // stencil_smi.cl:26-29,183-224).
     const bool overlap = g_tune.overlap != 0;
+    // CU partition (smi_stencil_set_bands): the band kernels and the exchange
+    // on band_cus reserved CUs, the interior on the rest in one round of
+    // waves; the caller's stream hands over to the pair and takes it back
+    const hipStream_t caller = s;
+    int reserve_waves = 0;
+    if (g_tune.band_cus > 0) {
+        int total = 0;
+        SMI_TRY(comm_cu_streams(c, g_tune.band_cus, &s, &cs, &total));
+        reserve_waves = std::max(1, resident_waves_of(plan.k[0] >= SWEEPK_MIN ? plan.k[0] : SWEEPK_MAX) *
+                                        g_tune.band_cus / total);
+        SMI_HIP_CHECK(hipEventRecord(ev_int, caller));
+        SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_int, 0));
+    }
     auto phase_start = [&]() -> int {
         SMI_HIP_CHECK(hipEventRecord(ev_int, s));
         SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
@@ -539,8 +552,8 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
                 bk.in = ak.in = bufp(cur);
                 bk.out = ak.out = bufp(cur ^ 1);
                 SMI_TRY(pass([&](hipStream_t st) { return launch_bandk(K, bk, st); },
-                             [&](hipStream_t st) { return launch_sweepk(K, ak, st); }, xchgk, p < npass - 1,
-                             ak.out));
+                             [&](hipStream_t st) { return launch_sweepk_ex(K, ak, 0, reserve_waves, true, st); },
+                             xchgk, p < npass - 1, ak.out));
             }
         } else if (K == 2) {
             // ---- pairs of steps (depth-2 halos)
@@ -576,9 +589,14 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             }
         }
     }
-    // the caller's stream owns the result: join the comm stream
+    // the caller's stream owns the result: join the comm stream (and the
+    // CU-masked main stream)
     SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-    SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
+    SMI_HIP_CHECK(hipStreamWaitEvent(caller, ev_edge, 0));
+    if (s != caller) {
+        SMI_HIP_CHECK(hipEventRecord(ev_int, s));
+        SMI_HIP_CHECK(hipStreamWaitEvent(caller, ev_int, 0));
+    }
     return SMI_SUCCESS;
 }
 

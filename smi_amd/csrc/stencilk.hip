@@ -35,6 +35,8 @@ static int resident_waves(int K) {
     }
 }
 
+int resident_waves_of(int K) { return resident_waves(K); }
+
 int sweepk_window_cols(int K) { return 256 - 8 * sweepk_apron_lanes(K); }
 
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) { return launch_sweepk_ex(K, a, 0, 0, true, s); }

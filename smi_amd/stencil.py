@@ -116,17 +116,18 @@ def get_tuning() -> dict:
                 overlap=v[3].value)
 
 
-def set_bands(band_rows: int = -1, interior_rounds: int = -1) -> None:
-    """Multi-rank K-step scheduling (bit-neutral): rows per left/right band
-    sub-window of the band kernel (0 = automatic) and rounds of resident waves
-    the interior sweep is cut into."""
-    _lib.call("smi_stencil_set_bands", band_rows, interior_rounds)
+def set_bands(band_cus: int = -1, interior_rounds: int = -1) -> None:
+    """Multi-rank K-step scheduling (bit-neutral): CUs reserved for the band
+    kernel and the exchange (0 = they share the GPU with the interior sweep)
+    and rounds of resident waves the interior sweep is cut into when they
+    share it.  -1 keeps a setting."""
+    _lib.call("smi_stencil_set_bands", band_cus, interior_rounds)
 
 
 def get_bands() -> dict:
     v = [ctypes.c_int() for _ in range(2)]
     _lib.call("smi_stencil_get_bands", *[ctypes.byref(x) for x in v])
-    return dict(band_rows=v[0].value, interior_rounds=v[1].value)
+    return dict(band_cus=v[0].value, interior_rounds=v[1].value)
 
 
 def set_fusion(steps_per_pass: int = 0, rows_per_wave: int = 0, rows_in_flight: int = 0) -> None:

@@ -350,23 +350,26 @@ def test_deep_decomposed(gpu, oracle_mod, k, pxpy, overlap):
 
 
 @pytest.mark.parametrize("k", [3, 7, 10, 12])
-@pytest.mark.parametrize("bands", [(1, 1), (5, 2), (24, 3), (1000, 2)])
+@pytest.mark.parametrize("bands", [(0, 1), (0, 3), (8, 1), (16, 2), (24, 1), (64, 1)])
 def test_band_tuning_is_bit_neutral(gpu, oracle_mod, k, bands):
-    """The band kernel's side sub-window height (1 row .. taller than the
-    tile) and the interior's rounds of resident waves change scheduling only:
-    a 3x3 decomposition (one interior rank with all eight neighbours) stays
-    bit-exact.  K = 7 and 10 have column bands (KC = 8, 12) wider than K."""
+    """CUs reserved for the bands and the exchange (a CU-masked stream pair,
+    or none) and the interior's rounds of resident waves change scheduling
+    only: a 3x3 decomposition (one interior rank with all eight neighbours)
+    stays bit-exact, with and without overlap.  K = 7 and 10 have column
+    bands (KC = 8, 12) wider than K."""
     from smi_amd import stencil
-    band_rows, rounds = bands
+    band_cus, rounds = bands
     old = stencil.get_bands()
-    stencil.set_bands(band_rows, rounds)
+    stencil.set_bands(band_cus, rounds)
     try:
-        g = oracle_mod.init_uniform(3 * 61, 3 * 140, seed=k + band_rows)
+        g = oracle_mod.init_uniform(3 * 61, 3 * 140, seed=k + band_cus)
         for T in (k, 2 * k + 1):
-            got = _run_fused(g, T, 3, 3, 1, k=k)
-            assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, bands, T)
+            for overlap in (1, 0):
+                got = _run_fused(g, T, 3, 3, overlap, k=k)
+                assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, bands, T, overlap)
+        assert stencil.get_bands() == dict(band_cus=band_cus, interior_rounds=rounds)
     finally:
-        stencil.set_bands(old["band_rows"], old["interior_rounds"])
+        stencil.set_bands(old["band_cus"], old["interior_rounds"])
 
 
 @pytest.mark.parametrize("k", [4, 8, 12])

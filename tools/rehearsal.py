@@ -12,8 +12,10 @@ are not the stencil's -- timing only.  Prints ms/step next to the plain
 single-tile run, i.e. an estimate of per-GPU weak-scaling efficiency with
 an exchange that costs one device-to-device copy of the halo bytes.
 REHEARSAL_ROUNDS (list) sets the rounds of resident waves the multi-rank
-interior sweep is cut into, REHEARSAL_BAND_ROWS (list) the rows per side-band
-sub-window of the band kernel (smi_stencil_set_bands; 0 = automatic).
+interior sweep is cut into, REHEARSAL_BAND_CUS (list) the CUs reserved for the
+band kernel and the exchange (smi_stencil_set_bands; 0 = shared GPU).
+REHEARSAL_PROF=0 times the runs without the library's profiling markers (the
+band / interior averages are then not reported).
 SMI_LOOPBACK_FUSED=1 prices the exchange as one copy kernel (like one RCCL
 group), SMI_LOOPBACK_NOXCHG=1 leaves it out.
 usage: rehearsal.py [tile] [K...]
@@ -44,7 +46,7 @@ def _timed(comm, t, sc, steps):
         stencil.run(comm, t, 2 * steps, 1, 1, sc)
         s.synchronize()
         profiling.reset()
-        profiling.enable(True)
+        profiling.enable(os.environ.get("REHEARSAL_PROF", "1") != "0")
         t0 = time.perf_counter()
         stencil.run(comm, t, steps, 1, 1, sc)
         s.synchronize()
@@ -67,9 +69,9 @@ def main():
         alone = timed(comm, t, sc, steps)[0]
         noxchg = os.environ.get("SMI_LOOPBACK_NOXCHG")
         grid = [(r, b) for r in (int(x) for x in os.environ.get("REHEARSAL_ROUNDS", "1,2,3").split(","))
-                for b in (int(x) for x in os.environ.get("REHEARSAL_BAND_ROWS", "0").split(","))]
-        for rounds, band_rows in grid:
-            stencil.set_bands(band_rows, rounds)
+                for b in (int(x) for x in os.environ.get("REHEARSAL_BAND_CUS", "0").split(","))]
+        for rounds, band_cus in grid:
+            stencil.set_bands(band_cus, rounds)
             for ov in [int(x) for x in os.environ.get("REHEARSAL_OVERLAP", "1,0").split(",")]:
                 stencil.set_tuning(overlap=ov)
                 os.environ["SMI_LOOPBACK"] = "1"
@@ -78,7 +80,7 @@ def main():
                 band = profiling.read(profiling.EDGE)
                 sweep = profiling.read(profiling.SWEEPK if k >= 4 else profiling.SWEEP)
                 os.environ.pop("SMI_LOOPBACK", None)
-                print(json.dumps({"K": k, "rounds": rounds, "band_rows": band_rows, "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
+                print(json.dumps({"K": k, "rounds": rounds, "band_cus": band_cus, "mask_layout": int(os.environ.get("SMI_REH_MASK_LAYOUT", "0")), "prof": os.environ.get("REHEARSAL_PROF", "1") != "0", "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
                                   "ms_per_step_alone": round(alone, 5),
                                   "ms_per_step_interior_rank": round(loop, 5),
                                   "efficiency": round(alone / loop, 4),

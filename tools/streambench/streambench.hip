@@ -1,0 +1,151 @@
+// streambench.hip -- cost of the two-stream pass schedule of a multi-rank
+// stencil run, without the stencil: per pass a long streaming kernel (the
+// interior stand-in: a 256 MiB copy) on the main stream and a short kernel
+// (the band stand-in) on a second stream, joined by cross-stream event waits
+// exactly as smi_stencil_run does.  Prints us per pass for each variant next
+// to the main-stream kernels alone, as JSON lines.
+//   streambench [passes]
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(2);                                                                 \
+        }                                                                            \
+    } while (0)
+
+__global__ void copy_kernel(const float4 *__restrict__ in, float4 *__restrict__ out, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
+// a few us of dependent VALU work per wave, no memory
+__global__ void small_kernel(float *out, int iters) {
+    float v = threadIdx.x;
+    for (int i = 0; i < iters; ++i) v = v * 1.0000001f + 0.5f;
+    if (v == -1.0f) out[threadIdx.x] = v;
+}
+
+struct Ctx {
+    float4 *a, *b;
+    size_t n;
+    float *sink;
+    hipStream_t s, cs;
+    hipEvent_t e_int, e_band;
+    uint32_t *f_int, *f_band;  // hipMallocSignalMemory counters (mode 7)
+};
+
+static void big(Ctx &c, int p) {
+    hipLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, c.s, p & 1 ? c.b : c.a, p & 1 ? c.a : c.b, c.n);
+}
+static void small(Ctx &c, hipStream_t st) { hipLaunchKernelGGL(small_kernel, dim3(800), dim3(64), 0, st, c.sink, 2000); }
+// the same launches with the completion event carried by the dispatch itself
+static void big_ev(Ctx &c, int p, hipEvent_t stop) {
+    hipExtLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, c.s, nullptr, stop, 0, p & 1 ? c.b : c.a,
+                          p & 1 ? c.a : c.b, c.n);
+}
+static void small_ev(Ctx &c, hipStream_t st, hipEvent_t stop) {
+    hipExtLaunchKernelGGL(small_kernel, dim3(800), dim3(64), 0, st, nullptr, stop, 0, c.sink, 2000);
+}
+
+// mode 0: big kernels alone; 1: + small kernel on cs, no dependencies;
+// 2: the stencil schedule (cs: [wait int(t-1)] small(t) rec band(t);
+//    s: big(t) rec int(t) [wait band(t)])
+// 3: as 2, the small kernel on the main stream before big (no second stream)
+// 4-6: the completion events carried by the kernel dispatches
+// (hipExtLaunchKernelGGL stop events), see run()
+// 7: as 2 with stream memory operations (write / wait value) for the joins
+static double run(Ctx &c, int mode, int passes) {
+    CK(hipDeviceSynchronize());
+    if (mode == 7) {  // counters restart at 0 (nothing pending on them now)
+        CK(hipStreamWriteValue32(c.s, c.f_int, 0u, 0));
+        CK(hipStreamWriteValue32(c.s, c.f_band, 0u, 0));
+        CK(hipDeviceSynchronize());
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    for (int p = 0; p < passes; ++p) {
+        if (mode == 0) {
+            big(c, p);
+        } else if (mode == 1) {
+            small(c, c.cs);
+            big(c, p);
+        } else if (mode == 2) {
+            small(c, c.cs);
+            CK(hipEventRecord(c.e_band, c.cs));
+            big(c, p);
+            CK(hipEventRecord(c.e_int, c.s));
+            CK(hipStreamWaitEvent(c.s, c.e_band, 0));
+            CK(hipStreamWaitEvent(c.cs, c.e_int, 0));
+        } else if (mode == 7) {
+            // as 2 with stream memory operations: monotone pass counters
+            small(c, c.cs);
+            CK(hipStreamWriteValue32(c.cs, c.f_band, (uint32_t)(p + 1), 0));
+            big(c, p);
+            CK(hipStreamWriteValue32(c.s, c.f_int, (uint32_t)(p + 1), 0));
+            CK(hipStreamWaitValue32(c.s, c.f_band, (uint32_t)(p + 1), hipStreamWaitValueGte, 0xFFFFFFFFu));
+            CK(hipStreamWaitValue32(c.cs, c.f_int, (uint32_t)(p + 1), hipStreamWaitValueGte, 0xFFFFFFFFu));
+        } else if (mode == 3) {
+            small(c, c.s);
+            big(c, p);
+        } else {
+            // 4: as 2 with dispatch-carried events; 5: without the main
+            // stream's wait; 6: without the second stream's wait
+            if (p > 0 && mode != 6) CK(hipStreamWaitEvent(c.cs, c.e_int, 0));
+            small_ev(c, c.cs, c.e_band);
+            if (p > 0 && mode != 5) CK(hipStreamWaitEvent(c.s, c.e_band, 0));
+            big_ev(c, p, c.e_int);
+        }
+    }
+    CK(hipStreamSynchronize(c.s));
+    CK(hipStreamSynchronize(c.cs));
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double, std::micro>(t1 - t0).count() / passes;
+}
+
+int main(int argc, char **argv) {
+    const int passes = argc > 1 ? atoi(argv[1]) : 200;
+    Ctx c;
+    c.n = (256u << 20) / 16;
+    CK(hipMalloc(&c.a, c.n * 16));
+    CK(hipMalloc(&c.b, c.n * 16));
+    CK(hipMalloc(&c.sink, 4096));
+    CK(hipMemset(c.a, 0, c.n * 16));
+    int can_wait = 0;
+    CK(hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, 0));
+    CK(hipExtMallocWithFlags((void **)&c.f_int, 8, hipMallocSignalMemory));
+    CK(hipExtMallocWithFlags((void **)&c.f_band, 8, hipMallocSignalMemory));
+    printf("{\"can_use_stream_wait_value\": %d}\n", can_wait);
+    int least, greatest;
+    CK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const char *evname[3] = {"default", "disable_timing", "disable_timing_sysfence"};
+    const unsigned evflags[3] = {hipEventDefault, hipEventDisableTiming,
+                                 hipEventDisableTiming | hipEventDisableSystemFence};
+    for (int prio = 1; prio < 2; ++prio) {
+        for (int ef = 1; ef < 3; ++ef) {
+            CK(hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking));
+            CK(hipStreamCreateWithPriority(&c.cs, hipStreamNonBlocking, prio ? greatest : least));
+            CK(hipEventCreateWithFlags(&c.e_int, evflags[ef]));
+            CK(hipEventCreateWithFlags(&c.e_band, evflags[ef]));
+            for (int mode = 0; mode < 8; ++mode) {
+                run(c, mode, 20);  // warm-up
+                const double us = run(c, mode, passes);
+                printf("{\"mode\": %d, \"comm_prio\": \"%s\", \"events\": \"%s\", \"us_per_pass\": %.2f}\n", mode,
+                       prio ? "high" : "low", evname[ef], us);
+                fflush(stdout);
+            }
+            CK(hipEventDestroy(c.e_int));
+            CK(hipEventDestroy(c.e_band));
+            CK(hipStreamDestroy(c.s));
+            CK(hipStreamDestroy(c.cs));
+        }
+    }
+    return 0;
+}
