@@ -95,6 +95,19 @@ int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in
 int smi_stencil_set_bands(int band_cus, int interior_rounds);
 int smi_stencil_get_bands(int *band_cus, int *interior_rounds);
 
+/* Multi-rank K-step passes, band placement.  fused = 1 (default, used when
+ * band_cus = 0): one launch per pass -- the interior sweep, some of whose
+ * waves first compute one band segment each (their own row blocks are
+ * balance_rows rows shorter) and count it in a device counter; the comm
+ * stream waits on the counter (hipStreamWaitValue32) and exchanges the new
+ * bands while the rest of the sweep runs, and the next pass waits for the
+ * exchange.  reserve_waves > 0: the sweep runs one round of waves minus that
+ * many, leaving slots for the exchange's kernels; 0: interior_rounds rounds.
+ * fused = 0: a separate band kernel on the comm stream beside the sweep.
+ * Pass < 0 to keep.  Scheduling only: bit-identical results. */
+int smi_stencil_set_band_fusion(int fused, int balance_rows, int reserve_waves);
+int smi_stencil_get_band_fusion(int *fused, int *balance_rows, int *reserve_waves);
+
 /* One phase of a planned run: `passes` launches of `steps_per_pass` steps. */
 typedef struct {
     int steps_per_pass;

@@ -130,6 +130,18 @@ int comm_cu_streams(Comm *c, int cus, hipStream_t *main, hipStream_t *band, int 
     return SMI_SUCCESS;
 }
 
+int comm_band_counter(Comm *c, unsigned **counter) {
+    if (!c->band_done) {
+        // fine-grained: a kernel's system-scope atomic on it releases work
+        // queued behind hipStreamWaitValue32 within a few us while the
+        // kernel still runs (signal memory took ~60 us, profiles/r03/trigger)
+        SMI_HIP_CHECK(hipExtMallocWithFlags((void **)&c->band_done, 64, hipDeviceMallocFinegrained));
+        SMI_HIP_CHECK(hipMemset(c->band_done, 0, 64));
+    }
+    *counter = c->band_done;
+    return SMI_SUCCESS;
+}
+
 static int finish_init(std::unique_ptr<Comm> c, SMI_Comm *out) {
     // highest priority: the ring kernels and the exchange it carries are on
     // the critical path, the interior sweep beside them is not
@@ -321,6 +333,7 @@ int smi_finalize(SMI_Comm comm) {
     if (c->work) SMI_HIP_CHECK(hipFree(c->work));
     if (c->halo) SMI_HIP_CHECK(hipFree(c->halo));
     if (c->comm_stream) SMI_HIP_CHECK(hipStreamDestroy(c->comm_stream));
+    if (c->band_done) SMI_HIP_CHECK(hipFree(c->band_done));
     if (c->band_stream) SMI_HIP_CHECK(hipStreamDestroy(c->band_stream));
     if (c->main_stream) SMI_HIP_CHECK(hipStreamDestroy(c->main_stream));
     return drain_rc;

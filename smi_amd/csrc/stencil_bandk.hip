@@ -19,7 +19,8 @@ SMI_BANDK_DECL(10)
 SMI_BANDK_DECL(11)
 SMI_BANDK_DECL(12)
 
-int launch_bandk(int K, BandKArgs a, hipStream_t s) {
+int plan_bands(int K, BandKArgs *ap) {
+    BandKArgs &a = *ap;
     const int X = a.rows, Y = a.cols;
     a.kc = kc_of(K);
     SMI_ARG_CHECK(K >= SWEEPK_MIN && K <= SWEEPK_MAX, "bandk: K must be 3..12");
@@ -37,6 +38,17 @@ int launch_bandk(int K, BandKArgs a, hipStream_t s) {
         n += waves_of[k];
     }
     a.first[4] = n;
+#ifdef SMI_LOOPBACK_REHEARSAL
+    // timing experiment: no band work at all (results are wrong)
+    if (getenv("SMI_REH_NOBANDS")) a.first[1] = a.first[2] = a.first[3] = a.first[4] = 0;
+    a.exp = getenv("SMI_REH_BANDEXP") ? atoi(getenv("SMI_REH_BANDEXP")) : 0;
+#endif
+    return SMI_SUCCESS;
+}
+
+int launch_bandk(int K, BandKArgs a, hipStream_t s) {
+    SMI_TRY(plan_bands(K, &a));
+    const int n = a.first[4];
     if (n == 0) return SMI_SUCCESS;
     int tok = -1;
     if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_EDGE, s, &tok, K));

@@ -80,6 +80,12 @@ struct Tuning {
     // (0: they share the whole GPU with the interior sweep; > 0: CU-masked
     // stream pair, the interior in one round of waves on the other CUs)
     int band_cus = 0;
+    // Fused multi-rank passes (default): the band segments run inside the
+    // interior sweep's launch (sweepk_fused_kernel) and a device counter
+    // releases the exchange mid-pass; 0: separate band kernel beside it.
+    int band_fused = 1;
+    int band_balance = 12;  // rows shorter: the row blocks of band-carrying waves (fused passes)
+    int band_reserve = 0;   // fused passes: wave slots left free for the exchange (0: rounds_multi rounds)
     int uk = 3;        // rows loaded ahead (K-step sweep: one 3-row register batch, fixed at build time)
 };
 extern Tuning g_tune;
@@ -160,8 +166,16 @@ struct BandKArgs {
     int first[5];      // first wave of band top, bottom, left, right; first[4] = all waves
     int sw;            // cells stored per wave (64 - 2K)
     int rlo, rhi;      // rows of the left/right bands
+#ifdef SMI_LOOPBACK_REHEARSAL
+    int exp;           // timing experiments (stencil_bandk.h), rehearsal build only
+#endif
 };
+int plan_bands(int K, BandKArgs *a);  // fills kc, first[], sw, rlo, rhi
 int launch_bandk(int K, BandKArgs a, hipStream_t s);
+// fused multi-rank pass: interior sweep + band segments (b planned), each
+// finished segment counted in *done (fine-grained memory); *segments = count
+int launch_sweepk_fused(int K, const SweepKArgs &a, const BandKArgs &b, int balance_rows, int reserve,
+                        unsigned *done, int *segments, hipStream_t s);
 int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s);
 
 }  // namespace smi

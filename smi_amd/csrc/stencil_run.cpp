@@ -288,6 +288,22 @@ int smi_stencil_get_bands(int *band_cus, int *interior_rounds) {
     return SMI_SUCCESS;
 }
 
+int smi_stencil_set_band_fusion(int fused, int balance_rows, int reserve_waves) {
+    SMI_ARG_CHECK(fused <= 1 && balance_rows <= 1024 && reserve_waves <= 65536,
+                  "fused / balance_rows / reserve_waves out of range");
+    if (fused >= 0) g_tune.band_fused = fused;
+    if (balance_rows >= 0) g_tune.band_balance = balance_rows;
+    if (reserve_waves >= 0) g_tune.band_reserve = reserve_waves;
+    return SMI_SUCCESS;
+}
+
+int smi_stencil_get_band_fusion(int *fused, int *balance_rows, int *reserve_waves) {
+    if (fused) *fused = g_tune.band_fused;
+    if (balance_rows) *balance_rows = g_tune.band_balance;
+    if (reserve_waves) *reserve_waves = g_tune.band_reserve;
+    return SMI_SUCCESS;
+}
+
 int smi_stencil_plan(int x_local, int y_local, int px, int py, int rank, int timesteps, SMI_StencilPhase *phases,
                      int max_phases, int *nphases, int *neighbours, int *result_index) {
     SMI_ARG_CHECK(x_local >= 1 && y_local >= 4 && y_local % 4 == 0, "tile must be >= 1 x 4, y_local % 4 == 0");
@@ -484,6 +500,9 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     // waves; the caller's stream hands over to the pair and takes it back
     const hipStream_t caller = s;
     int reserve_waves = 0;
+    // fused passes: wave slots the interior leaves free for the exchange's
+    // kernels (smi_stencil_set_band_fusion)
+    const int reserve_fused = g_tune.band_reserve;
     if (g_tune.band_cus > 0) {
         int total = 0;
         SMI_TRY(comm_cu_streams(c, g_tune.band_cus, &s, &cs, &total));
@@ -548,6 +567,40 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             };
             SMI_TRY(launch_packk(bufp(cur), rows, cols, K, hkv, cs));
             SMI_TRY(xchgk(bufp(cur), cs));
+            if (g_tune.band_fused && g_tune.band_cus == 0) {
+                // Fused passes: one launch per pass on the main stream (the
+                // interior sweep, whose band-carrying waves count their
+                // segments in a device counter); the comm stream waits on the
+                // counter, not on the launch, so the exchange of pass t runs
+                // beside the rest of its sweep, and pass t+1 waits for it:
+                //   comm : [counter >= segments(0..t)] exchange(t) -> rec E_x(t)
+                //   main : [wait E_x(t-1)] fused(t)
+                unsigned *done = nullptr;
+                SMI_TRY(comm_band_counter(c, &done));
+                SMI_HIP_CHECK(hipStreamWriteValue32(cs, done, 0u, 0));
+                SMI_TRY(plan_bands(K, &bk));
+                unsigned expect = 0;
+                for (int p = 0; p < npass; ++p, cur ^= 1) {
+                    bk.in = ak.in = bufp(cur);
+                    bk.out = ak.out = bufp(cur ^ 1);
+                    SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
+                    SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
+                    int segs = 0;
+                    SMI_TRY(launch_sweepk_fused(K, ak, bk, g_tune.band_balance, overlap ? reserve_fused : 0, done,
+                                                &segs, s));
+                    expect += (unsigned)segs;
+                    if (p == npass - 1) break;
+                    if (overlap) {
+                        SMI_HIP_CHECK(hipStreamWaitValue32(cs, done, expect, hipStreamWaitValueGte, 0xFFFFFFFFu));
+                    } else {
+                        SMI_HIP_CHECK(hipEventRecord(ev_int, s));
+                        SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
+                    }
+                    SMI_TRY(xchgk(ak.out, cs));
+                }
+                cur ^= 1;  // the loop's break skipped the last flip
+                continue;
+            }
             for (int p = 0; p < npass; ++p, cur ^= 1) {
                 bk.in = ak.in = bufp(cur);
                 bk.out = ak.out = bufp(cur ^ 1);

@@ -41,31 +41,38 @@ int sweepk_window_cols(int K) { return 256 - 8 * sweepk_apron_lanes(K); }
 
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) { return launch_sweepk_ex(K, a, 0, 0, true, s); }
 
+#define SMI_FUSED_DECL(K)                                                                                \
+    int sweepk_fused_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, const BandKArgs &b, int ds,  \
+                                 unsigned *done, int blocks, hipStream_t s);
+SMI_FUSED_DECL(3)
+SMI_FUSED_DECL(4)
+SMI_FUSED_DECL(5)
+SMI_FUSED_DECL(6)
+SMI_FUSED_DECL(7)
+SMI_FUSED_DECL(8)
+SMI_FUSED_DECL(9)
+SMI_FUSED_DECL(10)
+SMI_FUSED_DECL(11)
+SMI_FUSED_DECL(12)
+
+// Strips and row blocks of a K-step sweep over a's output rectangle.
 // ht > 0: rows per wave as given; else automatic (g_tune.htk, or one round
 // of resident waves -- minus `reserve` waves left to the comm stream's
-// kernels in a multi-rank run).  prof: record the launch under
-// SMI_PROF_STENCIL_SWEEPK (the ring's band sweeps are recorded by their
-// caller instead).
-int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool prof, hipStream_t s) {
-    if (a.row_hi <= a.row_lo || a.col_hi <= a.col_lo) return SMI_SUCCESS;
-    SMI_ARG_CHECK(K >= SWEEPK_MIN && K <= SWEEPK_MAX, "sweepk: steps per pass must be 3..12");
-    SMI_ARG_CHECK(a.cols % 4 == 0 && a.col_lo % 4 == 0 && a.col_hi % 4 == 0, "sweepk: columns not float4 aligned");
-    SMI_ARG_CHECK(a.row_lo >= 0 && a.row_hi <= a.rows && a.col_lo >= 0 && a.col_hi <= a.cols,
-                  "sweepk: output rectangle outside the tile");
+// kernels in a multi-rank run).
+static void sweepk_geometry(int K, const SweepKArgs &a, int ht_req, int reserve, int *nstrips_, int *nrb_) {
     const int sw = sweepk_window_cols(K);
-    const int nstrips = (a.col_hi - a.col_lo + sw - 1) / sw;
+    const int nstrips = (a.col_hi - (a.col_lo & ~31) + sw - 1) / sw;  // line-aligned strips (stencilk.h)
     const int out_rows = a.row_hi - a.row_lo;
     int ht = ht_req > 0 ? ht_req : g_tune.htk;
     if (ht <= 0) {
         // auto: one round of resident waves, each a tall row block of its
         // strip.  Multi-rank interior: either leave `reserve` waves to the
-        // ring's band sweeps and the exchange on the comm stream (one round
-        // of the rest), or cut the interior into several rounds so that
-        // workgroups retire during the pass and the comm stream's kernels are
-        // dispatched then.
+        // comm stream's kernels (one round of the rest), or cut the interior
+        // into several rounds so that workgroups retire during the pass and
+        // the comm stream's kernels are dispatched then.
         int waves = resident_waves(K);
 #ifdef SMI_LOOPBACK_REHEARSAL
-        // experiment: leave a share of the wave slots to the ring kernel
+        // experiment: leave a share of the wave slots to the band kernel
         if (const char *e = getenv("SMI_INTERIOR_PCT"))
             if (!(a.gT && a.gB && a.gL && a.gR)) waves = std::max(1, waves * atoi(e) / 100);
 #endif
@@ -78,16 +85,32 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
         const int per_strip = std::max(1, waves * rounds / nstrips);
         ht = std::max(2 * K, (out_rows + per_strip - 1) / per_strip);
     }
-    const int nrb = (out_rows + ht - 1) / ht;
+    *nstrips_ = nstrips;
+    *nrb_ = (out_rows + ht - 1) / ht;
+}
+
+static int check_sweepk(int K, const SweepKArgs &a) {
+    SMI_ARG_CHECK(K >= SWEEPK_MIN && K <= SWEEPK_MAX, "sweepk: steps per pass must be 3..12");
+    SMI_ARG_CHECK(a.cols % 4 == 0 && a.col_lo % 4 == 0 && a.col_hi % 4 == 0, "sweepk: columns not float4 aligned");
+    SMI_ARG_CHECK(a.row_lo >= 0 && a.row_hi <= a.rows && a.col_lo >= 0 && a.col_hi <= a.cols,
+                  "sweepk: output rectangle outside the tile");
+    return SMI_SUCCESS;
+}
+
+// prof: record the launch under SMI_PROF_STENCIL_SWEEPK
+int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool prof, hipStream_t s) {
+    if (a.row_hi <= a.row_lo || a.col_hi <= a.col_lo) return SMI_SUCCESS;
+    SMI_TRY(check_sweepk(K, a));
+    int nstrips = 0, nrb = 0;
+    sweepk_geometry(K, a, ht_req, reserve, &nstrips, &nrb);
+    const int out_rows = a.row_hi - a.row_lo;
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
     int tok = -1;
     // chained markers: within one smi_stencil_run (which restarts the
     // chain) back-to-back single-tile sweeps are timed from the end of the
     // previous one (one marker per pass).  The chain holds only while nothing
-    // else was recorded in between: in a multi-rank run with overlap the band
-    // kernel's markers on the comm stream break it, so each interior sweep
-    // gets its own begin marker and its time is its own duration.
+    // else was recorded in between (a multi-rank pass records on two streams).
     if (prof && prof_enabled())
         SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K,
                            true));
@@ -103,6 +126,49 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
     case 10: rc = sweepk_launch_k10(a, nstrips, nrb, blocks, s); break;
     case 11: rc = sweepk_launch_k11(a, nstrips, nrb, blocks, s); break;
     default: rc = sweepk_launch_k12(a, nstrips, nrb, blocks, s); break;
+    }
+    SMI_TRY(rc);
+    if (tok >= 0) SMI_TRY(prof_end(tok, s));
+    return SMI_SUCCESS;
+}
+
+// A fused multi-rank pass (stencil_bandk.h, sweepk_fused_kernel): the
+// interior sweep of `a` whose waves also compute the band segments of `b`
+// (b planned by plan_bands), each counted in `done` when finished.
+// balance_rows: how many rows shorter the row blocks of the band-carrying
+// waves are (0: segments dealt to the first waves, no balancing).  Returns
+// the number of band segments (the counter's increment) in *segments.
+int launch_sweepk_fused(int K, const SweepKArgs &a, const BandKArgs &b, int balance_rows, int reserve,
+                        unsigned *done, int *segments, hipStream_t s) {
+    SMI_TRY(check_sweepk(K, a));
+    const int nb = b.first[4];
+    *segments = nb;
+    int nstrips = 1, nrb = 0;
+    if (a.row_hi > a.row_lo && a.col_hi > a.col_lo) sweepk_geometry(K, a, 0, reserve, &nstrips, &nrb);
+    const long tasks = (long)nstrips * nrb;
+    // balanced only while every strip has enough row blocks for its share
+    // of segments and the short blocks stay >= 2K rows
+    const int out_rows = a.row_hi - a.row_lo;
+    int ds = balance_rows;
+    if (nb > tasks || (nrb > 0 && out_rows / nrb - ds < 2 * K)) ds = 0;
+    const long waves = ds > 0 ? tasks : std::max<long>(tasks, nb);
+    const int blocks = (int)((waves + 3) / 4);
+    if (blocks == 0) return SMI_SUCCESS;
+    int tok = -1;
+    if (prof_enabled())
+        SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)a.rows * a.cols * K, true));
+    int rc = SMI_SUCCESS;
+    switch (K) {
+    case 3: rc = sweepk_fused_launch_k3(a, nstrips, nrb, b, ds, done, blocks, s); break;
+    case 4: rc = sweepk_fused_launch_k4(a, nstrips, nrb, b, ds, done, blocks, s); break;
+    case 5: rc = sweepk_fused_launch_k5(a, nstrips, nrb, b, ds, done, blocks, s); break;
+    case 6: rc = sweepk_fused_launch_k6(a, nstrips, nrb, b, ds, done, blocks, s); break;
+    case 7: rc = sweepk_fused_launch_k7(a, nstrips, nrb, b, ds, done, blocks, s); break;
+    case 8: rc = sweepk_fused_launch_k8(a, nstrips, nrb, b, ds, done, blocks, s); break;
+    case 9: rc = sweepk_fused_launch_k9(a, nstrips, nrb, b, ds, done, blocks, s); break;
+    case 10: rc = sweepk_fused_launch_k10(a, nstrips, nrb, b, ds, done, blocks, s); break;
+    case 11: rc = sweepk_fused_launch_k11(a, nstrips, nrb, b, ds, done, blocks, s); break;
+    default: rc = sweepk_fused_launch_k12(a, nstrips, nrb, b, ds, done, blocks, s); break;
     }
     SMI_TRY(rc);
     if (tok >= 0) SMI_TRY(prof_end(tok, s));

@@ -372,6 +372,30 @@ def test_band_tuning_is_bit_neutral(gpu, oracle_mod, k, bands):
         stencil.set_bands(old["band_cus"], old["interior_rounds"])
 
 
+@pytest.mark.parametrize("k", [3, 8, 12])
+@pytest.mark.parametrize("fusion", [(0, 0, 0), (1, 0, 0), (1, 12, 0), (1, 40, 0), (1, 12, 64), (1, 0, 500)])
+def test_band_fusion_is_bit_neutral(gpu, oracle_mod, k, fusion):
+    """Bands as a separate kernel, or fused into the interior sweep's launch
+    with the exchange released by the device counter: unbalanced, balanced
+    (row blocks of band-carrying waves 12 / 40 rows shorter -- 40 falls back
+    to unbalanced on short blocks), one round minus reserved wave slots.  A
+    3x3 decomposition (an interior rank) with and without overlap and the
+    2x4 of the driver's 8-GPU run stay bit-exact."""
+    from smi_amd import stencil
+    old = stencil.get_band_fusion()
+    stencil.set_band_fusion(*fusion)
+    try:
+        assert stencil.get_band_fusion() == dict(fused=fusion[0], balance_rows=fusion[1], reserve_waves=fusion[2])
+        for PX, PY, X, Y in ((3, 3, 3 * 301, 3 * 700), (2, 4, 2 * 96, 4 * 128)):
+            g = oracle_mod.init_uniform(X, Y, seed=k + fusion[1] + PX)
+            for T in (2 * k, 2 * k + 1):
+                for overlap in (1, 0):
+                    got = _run_fused(g, T, PX, PY, overlap, k=k)
+                    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, fusion, PX, PY, T, overlap)
+    finally:
+        stencil.set_band_fusion(old["fused"], old["balance_rows"], old["reserve_waves"])
+
+
 @pytest.mark.parametrize("k", [4, 8, 12])
 def test_deep_decomposed_small_tiles(gpu, oracle_mod, k):
     # exactly 2K x 2K tiles (smallest deep tile), ring blocks larger than tiles

@@ -14,6 +14,8 @@ an exchange that costs one device-to-device copy of the halo bytes.
 REHEARSAL_ROUNDS (list) sets the rounds of resident waves the multi-rank
 interior sweep is cut into, REHEARSAL_BAND_CUS (list) the CUs reserved for the
 band kernel and the exchange (smi_stencil_set_bands; 0 = shared GPU).
+REHEARSAL_BANDFUSION (list of fused:balance_rows:reserve_waves, default
+1:12:0) the band placement (smi_stencil_set_band_fusion).
 REHEARSAL_PROF=0 times the runs without the library's profiling markers (the
 band / interior averages are then not reported).
 SMI_LOOPBACK_FUSED=1 prices the exchange as one copy kernel (like one RCCL
@@ -64,23 +66,32 @@ def main():
     sc = torch.empty_like(t)
     for k in ks:
         stencil.set_fusion(k)
-        steps = 10 * max(k, 2)
+        steps = int(os.environ.get("REHEARSAL_PASSES", "10")) * max(k, 2)
         os.environ.pop("SMI_LOOPBACK", None)
         alone = timed(comm, t, sc, steps)[0]
         noxchg = os.environ.get("SMI_LOOPBACK_NOXCHG")
         grid = [(r, b) for r in (int(x) for x in os.environ.get("REHEARSAL_ROUNDS", "1,2,3").split(","))
                 for b in (int(x) for x in os.environ.get("REHEARSAL_BAND_CUS", "0").split(","))]
-        for rounds, band_cus in grid:
+        fusions = [tuple(int(v) for v in f.split(":"))
+                   for f in os.environ.get("REHEARSAL_BANDFUSION", "1:12:0").split(",")]
+        grid = [(r, b, f) for r, b in grid for f in fusions]
+        for rounds, band_cus, fusion in grid:
             stencil.set_bands(band_cus, rounds)
+            stencil.set_band_fusion(*fusion)
             for ov in [int(x) for x in os.environ.get("REHEARSAL_OVERLAP", "1,0").split(",")]:
                 stencil.set_tuning(overlap=ov)
+                # the lone tile right before each setting (the GPU clock
+                # drifts between settings and boxes)
+                os.environ.pop("SMI_LOOPBACK", None)
+                alone = min(alone, timed(comm, t, sc, steps)[0]) if os.environ.get("REHEARSAL_ALONE_MIN") else \
+                    timed(comm, t, sc, steps)[0]
                 os.environ["SMI_LOOPBACK"] = "1"
                 runs = timed(comm, t, sc, steps)
                 loop = runs[0]
                 band = profiling.read(profiling.EDGE)
                 sweep = profiling.read(profiling.SWEEPK if k >= 4 else profiling.SWEEP)
                 os.environ.pop("SMI_LOOPBACK", None)
-                print(json.dumps({"K": k, "rounds": rounds, "band_cus": band_cus, "mask_layout": int(os.environ.get("SMI_REH_MASK_LAYOUT", "0")), "prof": os.environ.get("REHEARSAL_PROF", "1") != "0", "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
+                print(json.dumps({"K": k, "rounds": rounds, "band_cus": band_cus, "band_fusion": list(fusion), "no_bands": bool(os.environ.get("SMI_REH_NOBANDS")), "mask_layout": int(os.environ.get("SMI_REH_MASK_LAYOUT", "0")), "prof": os.environ.get("REHEARSAL_PROF", "1") != "0", "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
                                   "ms_per_step_alone": round(alone, 5),
                                   "ms_per_step_interior_rank": round(loop, 5),
                                   "efficiency": round(alone / loop, 4),
