@@ -84,29 +84,14 @@ int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
 int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_flight);
 int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in_flight);
 
-/* Multi-rank K-step passes: band_cus = CUs reserved for the band kernel and
- * the halo exchange (0..128; 0 = they share the whole GPU with the interior
- * sweep; > 0 = a CU-masked stream pair, the same number of CUs reserved on
- * every XCD -- use multiples of 8 -- and the interior sweep in one round of
- * waves on the other CUs); interior_rounds = rounds of resident waves the
- * interior sweep is cut into when they share the GPU (workgroups retire
- * mid-pass, so the band kernel and RCCL kernels find slots).  Pass < 0 to
- * keep.  Scheduling only: bit-identical results for every setting. */
-int smi_stencil_set_bands(int band_cus, int interior_rounds);
-int smi_stencil_get_bands(int *band_cus, int *interior_rounds);
-
-/* Multi-rank K-step passes, band placement.  fused = 1 (default, used when
- * band_cus = 0): one launch per pass -- the interior sweep, some of whose
- * waves first compute one band segment each (their own row blocks are
- * balance_rows rows shorter) and count it in a device counter; the comm
- * stream waits on the counter (hipStreamWaitValue32) and exchanges the new
- * bands while the rest of the sweep runs, and the next pass waits for the
- * exchange.  reserve_waves > 0: the sweep runs one round of waves minus that
- * many, leaving slots for the exchange's kernels; 0: interior_rounds rounds.
- * fused = 0: a separate band kernel on the comm stream beside the sweep.
- * Pass < 0 to keep.  Scheduling only: bit-identical results. */
-int smi_stencil_set_band_fusion(int fused, int balance_rows, int reserve_waves);
-int smi_stencil_get_band_fusion(int *fused, int *balance_rows, int *reserve_waves);
+/* Multi-rank K-step passes: the interior sweep runs beside the band kernel
+ * (the halo-facing bands, on the comm stream) and the exchange.
+ * reserve_waves = wave slots the interior sweep leaves free for them (0 =
+ * none: the band kernel fills the interior's tail), interior_rounds =
+ * rounds of resident waves the interior sweep is cut into (default 1).  Pass
+ * < 0 to keep.  Scheduling only: bit-identical results for every setting. */
+int smi_stencil_set_bands(int reserve_waves, int interior_rounds);
+int smi_stencil_get_bands(int *reserve_waves, int *interior_rounds);
 
 /* One phase of a planned run: `passes` launches of `steps_per_pass` steps. */
 typedef struct {

@@ -273,7 +273,6 @@ int smi_reduce(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count, 
         return launch_fold(rows, recvbuf, 1, count, type, op, s);
     }
     const size_t cs = chunk_elems(count, n, esz);
-    const size_t my_len = chunk_len(count, cs, me);
     const Pieces pc = pieces_of(cs, esz);
     // workspace: two exchange slots of n staging rows, plus the reduced
     // chunk of a non-root owner (cs elements).  Rows sit kStagePad bytes

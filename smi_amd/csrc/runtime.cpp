@@ -9,9 +9,6 @@
 #include <unordered_map>
 
 #include <cstdlib>
-#include <vector>
-
-#include <hip/hip_ext.h>
 
 #include "smi_internal.h"
 
@@ -76,69 +73,6 @@ int comm_event(Comm *c, int idx, hipEvent_t *ev) {
         c->events.push_back(e);
     }
     *ev = c->events[idx];
-    return SMI_SUCCESS;
-}
-
-// CU masks (hipExtStreamCreateWithCUMask): bit i of the mask enables CU i of
-// the driver's numbering, which interleaves the XCDs (bit i -> XCD i mod 8 on
-// an 8-XCD MI355X, then shader engine, then CU), so the top `cus` bits, cus
-// a multiple of 8, reserve the same number of CUs on every XCD and the
-// complement keeps every XCD's L2 equally fed for the interior sweep, whose
-// blocks are dealt to the XCDs round-robin.
-static void cu_masks(int total, int cus, std::vector<uint32_t> *band, std::vector<uint32_t> *rest) {
-    const int words = (total + 31) / 32;
-    band->assign(words, 0u);
-    rest->assign(words, 0u);
-#ifdef SMI_LOOPBACK_REHEARSAL
-    // experiment: the last cus / 8 bits of each 32-bit word instead (the
-    // even spread if the numbering were XCD-major instead)
-    const bool per_word = getenv("SMI_REH_MASK_LAYOUT") && atoi(getenv("SMI_REH_MASK_LAYOUT")) == 1;
-#else
-    const bool per_word = false;
-#endif
-    for (int i = 0; i < total; ++i) {
-        const bool reserved = per_word ? (i % 32) >= 32 - cus / std::max(1, words) : i >= total - cus;
-        (reserved ? *band : *rest)[i / 32] |= 1u << (i % 32);
-    }
-}
-
-int comm_cu_streams(Comm *c, int cus, hipStream_t *main, hipStream_t *band, int *total) {
-    int n = 0;
-    SMI_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, c->device));
-    SMI_ARG_CHECK(cus > 0 && cus < n, "band CUs must be 1 .. CUs - 1");
-    if (c->band_cus != cus) {
-        if (c->band_stream) {
-            SMI_HIP_CHECK(hipStreamSynchronize(c->band_stream));
-            SMI_HIP_CHECK(hipStreamDestroy(c->band_stream));
-            c->band_stream = nullptr;
-        }
-        if (c->main_stream) {
-            SMI_HIP_CHECK(hipStreamSynchronize(c->main_stream));
-            SMI_HIP_CHECK(hipStreamDestroy(c->main_stream));
-            c->main_stream = nullptr;
-        }
-        c->band_cus = 0;
-        std::vector<uint32_t> mb, mr;
-        cu_masks(n, cus, &mb, &mr);
-        SMI_HIP_CHECK(hipExtStreamCreateWithCUMask(&c->band_stream, (uint32_t)mb.size(), mb.data()));
-        SMI_HIP_CHECK(hipExtStreamCreateWithCUMask(&c->main_stream, (uint32_t)mr.size(), mr.data()));
-        c->band_cus = cus;
-    }
-    *main = c->main_stream;
-    *band = c->band_stream;
-    *total = n;
-    return SMI_SUCCESS;
-}
-
-int comm_band_counter(Comm *c, unsigned **counter) {
-    if (!c->band_done) {
-        // fine-grained: a kernel's system-scope atomic on it releases work
-        // queued behind hipStreamWaitValue32 within a few us while the
-        // kernel still runs (signal memory took ~60 us, profiles/r03/trigger)
-        SMI_HIP_CHECK(hipExtMallocWithFlags((void **)&c->band_done, 64, hipDeviceMallocFinegrained));
-        SMI_HIP_CHECK(hipMemset(c->band_done, 0, 64));
-    }
-    *counter = c->band_done;
     return SMI_SUCCESS;
 }
 
@@ -333,9 +267,6 @@ int smi_finalize(SMI_Comm comm) {
     if (c->work) SMI_HIP_CHECK(hipFree(c->work));
     if (c->halo) SMI_HIP_CHECK(hipFree(c->halo));
     if (c->comm_stream) SMI_HIP_CHECK(hipStreamDestroy(c->comm_stream));
-    if (c->band_done) SMI_HIP_CHECK(hipFree(c->band_done));
-    if (c->band_stream) SMI_HIP_CHECK(hipStreamDestroy(c->band_stream));
-    if (c->main_stream) SMI_HIP_CHECK(hipStreamDestroy(c->main_stream));
     return drain_rc;
 }
 

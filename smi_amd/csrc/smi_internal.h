@@ -123,24 +123,12 @@ struct Comm {
     size_t halo_elems = 0;
     std::vector<hipEvent_t> events;  // reusable sync events
     std::shared_ptr<void> chan_engine;  // element-granular channels (channels.cpp)
-    // CU-partitioned stream pair of multi-rank stencil runs
-    // (smi_stencil_set_bands): band_stream runs on band_cus reserved CUs,
-    // main_stream on the rest of the GPU; created on first use.
-    hipStream_t band_stream = nullptr, main_stream = nullptr;
-    int band_cus = 0;
-    // fused multi-rank passes: count of finished band segments, fine-grained
-    // device memory the comm stream waits on (hipStreamWaitValue32)
-    unsigned *band_done = nullptr;
 };
 
 Comm *lookup_comm(SMI_Comm c);
 int comm_workspace(Comm *c, size_t bytes, void **ptr);
 int comm_event(Comm *c, int idx, hipEvent_t *ev);
-// The CU-partitioned stream pair of `c` for `cus` reserved CUs (created or
-// re-created when `cus` changed); *total = the device's CU count.
-int comm_cu_streams(Comm *c, int cus, hipStream_t *main, hipStream_t *band, int *total);
-// The band-segment counter of `c` (allocated on first use).
-int comm_band_counter(Comm *c, unsigned **counter);
+
 // Wait until every detached channel send of `c` has been received (finalize).
 int channels_drain(Comm *c);
 

@@ -91,54 +91,6 @@ struct BandSrc {
     }
 };
 
-// Band stores.  WT (fused passes): write-through to memory (buffer stores
-// with sc0 sc1), so that after its own stores have completed (s_waitcnt) a
-// wave can signal the comm stream without an L2 writeback: the exchange's
-// kernels may run on any XCD, and a release fence at agent scope writes back
-// the whole L2 of the wave's XCD (buffer_wbl2) -- one per band wave cost the
-// fused pass ~50 % (profiles/r03/).  `base` is wave-uniform, `off` the lane's
-// byte offset from it (< 2 GiB).
-// Timing experiments of the rehearsal build (BandKArgs::exp, set from
-// SMI_REH_BANDEXP by plan_bands; results are wrong): bit 0 no band stores,
-// bit 1 cached stores instead of write-through, bit 2 no band loads.
-#ifdef SMI_LOOPBACK_REHEARSAL
-#define SMI_BAND_EXP_OF(a) ((a).exp)
-#else
-#define SMI_BAND_EXP_OF(a) 0
-#endif
-
-template <bool WT>
-__device__ __forceinline__ void band_store(float *base, unsigned off, float v, int exp = 0) {
-    if (exp & 1) return;
-    if (WT && (exp & 2)) {
-        *reinterpret_cast<float *>(reinterpret_cast<char *>(base) + off) = v;
-        return;
-    }
-    if constexpr (WT) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, (int)off, 0, 17 /* sc0 sc1 */);
-    } else {
-        *reinterpret_cast<float *>(reinterpret_cast<char *>(base) + off) = v;
-    }
-}
-template <bool WT>
-__device__ __forceinline__ void band_store4(float *base, unsigned off, const float4 &v, int exp = 0) {
-    if (exp & 1) return;
-    if (WT && (exp & 2)) {
-        *reinterpret_cast<float4 *>(reinterpret_cast<char *>(base) + off) = v;
-        return;
-    }
-    if constexpr (WT) {
-        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
-        const u4 d = {__builtin_bit_cast(unsigned, v.x), __builtin_bit_cast(unsigned, v.y),
-                      __builtin_bit_cast(unsigned, v.z), __builtin_bit_cast(unsigned, v.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)off, 0, 17 /* sc0 sc1 */);
-    } else {
-        *reinterpret_cast<float4 *>(reinterpret_cast<char *>(base) + off) = v;
-    }
-}
-
 template <int K>
 struct BandW {
     static constexpr int KC = kc_of(K);
@@ -173,7 +125,7 @@ struct BandW {
     }
 
     // top (BOT = false) or bottom band: lane = column c, rows r0 + t
-    template <bool BOT, bool CP, bool WT>
+    template <bool BOT, bool CP>
     __device__ __forceinline__ static void rows(const BandKArgs &a, int w, int lane) {
         const int X = a.rows, Y = a.cols;
         const int c = w * SW - K + lane;
@@ -191,10 +143,6 @@ struct BandW {
         static_for<NR>([&](auto T) {
             constexpr int t = T;
             constexpr bool halo = BOT ? t >= 2 * K : t < K;
-            if (SMI_BAND_EXP_OF(a) & 4) {
-                x[t] = (float)(t + lane);
-                return;
-            }
             x[t] = halo ? ph[(t - th) * sh] : pt[(t - tt) * st];
         });
         const bool store = lane >= K && lane < 64 - K && c < Y;
@@ -204,22 +152,22 @@ struct BandW {
             constexpr int q = Q;  // output row r0 + K + q
             if (!store) return;
             const int r = r0 + K + q;
-            band_store<WT>(a.out + (size_t)r * Y, 4u * c, v, SMI_BAND_EXP_OF(a));
+            a.out[(size_t)r * Y + c] = v;
             if (!a.pack) return;
             // tee: packed side columns and this band's two K x KC corner blocks
             if (c < KCr) {
-                band_store<WT>(a.h.send_left, 4u * (r * KCr + c), v, SMI_BAND_EXP_OF(a));
-                band_store<WT>(a.h.send_corner[BOT ? 2 : 0], 4u * (q * KCr + c), v, SMI_BAND_EXP_OF(a));
+                a.h.send_left[(size_t)r * KCr + c] = v;
+                a.h.send_corner[BOT ? 2 : 0][q * KCr + c] = v;
             }
             if (c >= Y - KCr) {
-                band_store<WT>(a.h.send_right, 4u * (r * KCr + c - (Y - KCr)), v, SMI_BAND_EXP_OF(a));
-                band_store<WT>(a.h.send_corner[BOT ? 3 : 1], 4u * (q * KCr + c - (Y - KCr)), v, SMI_BAND_EXP_OF(a));
+                a.h.send_right[(size_t)r * KCr + c - (Y - KCr)] = v;
+                a.h.send_corner[BOT ? 3 : 1][q * KCr + c - (Y - KCr)] = v;
             }
         });
     }
 
     // left (RIGHT = false) or right band: lane = row r, columns c0 + t
-    template <bool RIGHT, bool CP, bool WT>
+    template <bool RIGHT, bool CP>
     __device__ __forceinline__ static void cols(const BandKArgs &a, int w, int lane) {
         const int X = a.rows, Y = a.cols;
         const int r = a.rlo + w * SW - K + lane;
@@ -230,10 +178,6 @@ struct BandW {
         float4 g[G4];
         static_for<G4>([&](auto G) {
             constexpr int j = G;
-            if (SMI_BAND_EXP_OF(a) & 4) {
-                g[j] = make_float4(j, lane, 1.0f, 2.0f);
-                return;
-            }
             g[j] = *reinterpret_cast<const float4 *>(src.at(r, g0 + 4 * j));
         });
         float x[NC];
@@ -249,19 +193,17 @@ struct BandW {
         if (!store) return;
         const int c0 = RIGHT ? Y - KC : 0;
         float *send = RIGHT ? a.h.send_right : a.h.send_left;
-        // the wave's rows are consecutive: offsets from its first lane's row
-        const int rw = __builtin_amdgcn_readfirstlane(r);
-        float *tile = a.out + (size_t)rw * Y + c0;
         static_for<KC / 4>([&](auto G) {
             constexpr int j = 4 * G;
             const float4 v = make_float4(o[j], o[j + 1], o[j + 2], o[j + 3]);
-            band_store4<WT>(tile, 4u * ((r - rw) * Y + j), v, SMI_BAND_EXP_OF(a));
+            *reinterpret_cast<float4 *>(a.out + (size_t)r * Y + c0 + j) = v;
             if (a.pack) {
-                band_store4<WT>(send, 4u * (r * KC + j), v, SMI_BAND_EXP_OF(a));
+                *reinterpret_cast<float4 *>(send + (size_t)r * KC + j) = v;
                 // corner blocks of rows this band owns (only when the top /
                 // bottom side is a global edge, i.e. never sent)
-                if (r < K) band_store4<WT>(a.h.send_corner[RIGHT ? 1 : 0], 4u * (r * KC + j), v, SMI_BAND_EXP_OF(a));
-                if (r >= X - K) band_store4<WT>(a.h.send_corner[RIGHT ? 3 : 2], 4u * ((r - (X - K)) * KC + j), v, SMI_BAND_EXP_OF(a));
+                if (r < K) *reinterpret_cast<float4 *>(a.h.send_corner[RIGHT ? 1 : 0] + r * KC + j) = v;
+                if (r >= X - K)
+                    *reinterpret_cast<float4 *>(a.h.send_corner[RIGHT ? 3 : 2] + (r - (X - K)) * KC + j) = v;
             }
         });
     }
@@ -270,7 +212,7 @@ struct BandW {
 // Band segment wv: one wave per 64-cell run of a band; segments [first[0],
 // first[1]) top, [first[1], first[2]) bottom, [first[2], first[3]) left,
 // [first[3], first[4]) right.
-template <int K, bool WT>
+template <int K>
 __device__ __forceinline__ void bandk_wave(const BandKArgs &a, int wv, int lane) {
     using B = BandW<K>;
     const int band = (wv >= a.first[1]) + (wv >= a.first[2]) + (wv >= a.first[3]);
@@ -282,16 +224,16 @@ __device__ __forceinline__ void bandk_wave(const BandKArgs &a, int wv, int lane)
         const int c_lo = w * B::SW - K, c_hi = c_lo + 63;
         const bool cp = (!a.has[2] && c_lo <= 0 && c_hi >= 0) || (!a.has[3] && c_lo <= Y - 1 && c_hi >= Y - 1);
         if (band == 0)
-            cp ? B::template rows<false, true, WT>(a, w, lane) : B::template rows<false, false, WT>(a, w, lane);
+            cp ? B::template rows<false, true>(a, w, lane) : B::template rows<false, false>(a, w, lane);
         else
-            cp ? B::template rows<true, true, WT>(a, w, lane) : B::template rows<true, false, WT>(a, w, lane);
+            cp ? B::template rows<true, true>(a, w, lane) : B::template rows<true, false>(a, w, lane);
     } else {
         const int r_lo = a.rlo + w * B::SW - K, r_hi = r_lo + 63;
         const bool cp = (!a.has[0] && r_lo <= 0 && r_hi >= 0) || (!a.has[1] && r_lo <= X - 1 && r_hi >= X - 1);
         if (band == 2)
-            cp ? B::template cols<false, true, WT>(a, w, lane) : B::template cols<false, false, WT>(a, w, lane);
+            cp ? B::template cols<false, true>(a, w, lane) : B::template cols<false, false>(a, w, lane);
         else
-            cp ? B::template cols<true, true, WT>(a, w, lane) : B::template cols<true, false, WT>(a, w, lane);
+            cp ? B::template cols<true, true>(a, w, lane) : B::template cols<true, false>(a, w, lane);
     }
 }
 
@@ -301,88 +243,12 @@ template <int K>
 __global__ __launch_bounds__(256) void bandk_kernel(BandKArgs a) {
     const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (int)(threadIdx.x >> 6));
     if (wv >= a.first[4]) return;  // wave-uniform
-    bandk_wave<K, false>(a, wv, threadIdx.x & 63);
-}
-
-// Fused multi-rank passes: which waves carry band segments.  Segment i goes
-// to the i-th wave in dispatch order (raw block index): those workgroups are
-// resident from the start of the pass (the launch leaves slots free for the
-// comm stream's kernels), so every segment is done early and the exchange
-// can start while the sweep runs.  xcd_remap deals raw blocks b, b+8, ... of
-// XCD x to the contiguous logical range starting at base(x), so the
-// band-carrying tasks form 8 contiguous task intervals, one per XCD -- the
-// band work is spread evenly over the XCDs.  band_short_count(rb, s) = how
-// many of row blocks [0, rb) of strip s belong to band-carrying waves (their
-// blocks are ds rows shorter, sweepk_block_row).
-__device__ __forceinline__ int band_short_count(int rb, int s, int nstrips, int nb, int nblocks) {
-    if (nb <= 0) return 0;
-    const int q = nblocks >> 3, r = nblocks & 7;
-    const int nbb = (nb + 3) / 4;               // band-carrying workgroups: raw blocks [0, nbb)
-    const int part = nb - 4 * (nbb - 1);        // waves of the last one (1..4)
-    const int xl = (nbb - 1) & 7;               // its XCD
-    int n = 0;
-    for (int x = 0; x < 8; ++x) {
-        const int m = x < nbb ? (nbb - x + 7) / 8 : 0;  // band blocks on XCD x
-        if (m == 0) continue;
-        const int base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-        const int t0 = 4 * base, t1 = t0 + 4 * m - (x == xl ? 4 - part : 0);  // band tasks [t0, t1)
-        // row blocks rb' of strip s with t0 <= rb' nstrips + s < t1
-        const int lo = t0 - s <= 0 ? 0 : (t0 - s + nstrips - 1) / nstrips;
-        const int hi = t1 - s <= 0 ? 0 : (t1 - s + nstrips - 1) / nstrips;
-        n += max(0, min(rb, hi) - lo);
-    }
-    return n;
-}
-
-// A fused multi-rank pass: the interior sweep, with the band segments as the
-// first work of the first nb waves in dispatch order, so that the bands need
-// no wave slots of their own and no second stream.  Their interior row
-// blocks are ds rows shorter (balance).  A wave's segment stores are
-// write-through and counted in `done` (fine-grained memory, system scope)
-// once they completed: the comm stream waits on that counter
-// (hipStreamWaitValue32) and starts the exchange of the bands while the
-// interior sweep runs -- the reference's Write kernel handing each boundary
-// row to the channels as it is produced (stencil_smi.cl:183-224).  When the
-// tile has fewer interior tasks than band segments (tiny tiles), ds = 0 and
-// the grid covers every segment.
-template <int K>
-__global__ __launch_bounds__(256) void sweepk_fused_kernel(SweepKArgs a, int nstrips, int nrb, BandKArgs b, int ds,
-                                                           unsigned *done) {
-    const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int lane = threadIdx.x & 63;
-    const int task = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
-    const int raw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-    const int nb = b.first[4];
-    const int rb = task / nstrips;
-    const int strip = task - rb * nstrips;
-    const int seg = raw < nb ? raw : -1;
-    // The segment's write-through stores have reached memory once they
-    // completed; the wave then counts it with one system-scope add (no L2
-    // writeback, see band_store) -- at the drain after its block's prologue,
-    // which waits for them anyway, or right here when it has no block.
-    if (seg >= 0) bandk_wave<K, true>(b, seg, lane);  // wave-uniform
-    if (rb < nrb) {
-        const int ns = ds > 0 ? band_short_count(nrb, strip, nstrips, nb, gridDim.x) : 0;
-        const int c0 = ds > 0 ? band_short_count(rb, strip, nstrips, nb, gridDim.x) : 0;
-        sweepk_task<K>(a, strip, rb, nrb, ns, ds, c0, lane, seg >= 0 ? done : nullptr);
-    } else if (seg >= 0) {
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (lane == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    bandk_wave<K>(a, wv, threadIdx.x & 63);
 }
 
 template <int K>
 int bandk_launch_impl(const BandKArgs &a, int waves, hipStream_t s) {
     hipLaunchKernelGGL((bandk_kernel<K>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
-    SMI_HIP_CHECK(hipGetLastError());
-    return SMI_SUCCESS;
-}
-
-template <int K>
-int sweepk_fused_launch_impl(const SweepKArgs &a, int nstrips, int nrb, const BandKArgs &b, int ds, unsigned *done,
-                             int blocks, hipStream_t s) {
-    hipLaunchKernelGGL((sweepk_fused_kernel<K>), dim3(blocks), dim3(256), 0, s, a, nstrips, nrb, b, ds, done);
     SMI_HIP_CHECK(hipGetLastError());
     return SMI_SUCCESS;
 }
@@ -393,9 +259,5 @@ int sweepk_fused_launch_impl(const SweepKArgs &a, int nstrips, int nrb, const Ba
     namespace smi {                                                                                      \
     int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s) {                                \
         return bandk_launch_impl<K>(a, waves, s);                                                        \
-    }                                                                                                    \
-    int sweepk_fused_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, const BandKArgs &b, int ds,  \
-                                 unsigned *done, int blocks, hipStream_t s) {                            \
-        return sweepk_fused_launch_impl<K>(a, nstrips, nrb, b, ds, done, blocks, s);                     \
     }                                                                                                    \
     }

@@ -41,7 +41,6 @@ int plan_bands(int K, BandKArgs *ap) {
 #ifdef SMI_LOOPBACK_REHEARSAL
     // timing experiment: no band work at all (results are wrong)
     if (getenv("SMI_REH_NOBANDS")) a.first[1] = a.first[2] = a.first[3] = a.first[4] = 0;
-    a.exp = getenv("SMI_REH_BANDEXP") ? atoi(getenv("SMI_REH_BANDEXP")) : 0;
 #endif
     return SMI_SUCCESS;
 }

@@ -69,23 +69,13 @@ struct Tuning {
     int ht2 = 8;        // rows per wave (two-step sweep)
     int u2 = 8;         // rows in flight per batch (two-step sweep)
     int htk = 0;        // rows per wave (K-step sweep, K >= 4); 0 = one round of resident waves
-    // K-step interior in multi-rank runs: rounds of resident waves.  One round
-    // hides the ring + a one-kernel exchange completely on the loopback
-    // rehearsal (0.997 of a lone tile), 2 rounds 0.985, 3 rounds 0.92
-    // (profiles/r01e/rehearsal_fused_exchange.log); 2 keeps a mid-pass point
-    // where workgroups retire, so the RCCL kernel of the exchange is never
-    // left without a slot until the interior ends.
-    int rounds_multi = 2;
-    // CUs reserved for the band kernel and the exchange of multi-rank runs
-    // (0: they share the whole GPU with the interior sweep; > 0: CU-masked
-    // stream pair, the interior in one round of waves on the other CUs)
-    int band_cus = 0;
-    // Fused multi-rank passes (default): the band segments run inside the
-    // interior sweep's launch (sweepk_fused_kernel) and a device counter
-    // releases the exchange mid-pass; 0: separate band kernel beside it.
-    int band_fused = 1;
-    int band_balance = 12;  // rows shorter: the row blocks of band-carrying waves (fused passes)
-    int band_reserve = 0;   // fused passes: wave slots left free for the exchange (0: rounds_multi rounds)
+    // K-step interior in multi-rank runs: rounds of resident waves, and
+    // wave slots left free for the band kernel and the exchange
+    // (smi_stencil_set_bands).  One round, none reserved: the interior-rank
+    // rehearsal runs at 0.87 of a lone tile with the band kernel in the
+    // interior's tail, 0.81-0.85 with two rounds (profiles/r03/).
+    int rounds_multi = 1;
+    int band_reserve = 0;
     int uk = 3;        // rows loaded ahead (K-step sweep: one 3-row register batch, fixed at build time)
 };
 extern Tuning g_tune;
@@ -137,7 +127,6 @@ __host__ __device__ constexpr int sweepk_apron_lanes(int K) { return K >= 9 ? 4 
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s);
 int launch_sweepk_ex(int K, const SweepKArgs &a, int ht, int reserve, bool prof, hipStream_t s);
 int sweepk_window_cols(int K);  // output columns per 256-column window
-int resident_waves_of(int K);   // waves of sweepk<K> one round of the whole GPU holds
 
 // Depth-K halos (stencil_bandk.h / stencil_bandk.hip).  KC = 4 ceil(K/4):
 // the column depth, whole float4 groups.  Receive side: top = rows -K..-1 and
@@ -166,16 +155,9 @@ struct BandKArgs {
     int first[5];      // first wave of band top, bottom, left, right; first[4] = all waves
     int sw;            // cells stored per wave (64 - 2K)
     int rlo, rhi;      // rows of the left/right bands
-#ifdef SMI_LOOPBACK_REHEARSAL
-    int exp;           // timing experiments (stencil_bandk.h), rehearsal build only
-#endif
 };
 int plan_bands(int K, BandKArgs *a);  // fills kc, first[], sw, rlo, rhi
 int launch_bandk(int K, BandKArgs a, hipStream_t s);
-// fused multi-rank pass: interior sweep + band segments (b planned), each
-// finished segment counted in *done (fine-grained memory); *segments = count
-int launch_sweepk_fused(int K, const SweepKArgs &a, const BandKArgs &b, int balance_rows, int reserve,
-                        unsigned *done, int *segments, hipStream_t s);
 int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s);
 
 }  // namespace smi

@@ -275,32 +275,16 @@ int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in
     return SMI_SUCCESS;
 }
 
-int smi_stencil_set_bands(int band_cus, int interior_rounds) {
-    SMI_ARG_CHECK(band_cus <= 128 && interior_rounds <= 64, "band_cus / interior_rounds out of range");
-    if (band_cus >= 0) g_tune.band_cus = band_cus;
+int smi_stencil_set_bands(int reserve_waves, int interior_rounds) {
+    SMI_ARG_CHECK(reserve_waves <= 65536 && interior_rounds <= 64, "reserve_waves / interior_rounds out of range");
+    if (reserve_waves >= 0) g_tune.band_reserve = reserve_waves;
     if (interior_rounds >= 0) g_tune.rounds_multi = std::max(1, interior_rounds);
     return SMI_SUCCESS;
 }
 
-int smi_stencil_get_bands(int *band_cus, int *interior_rounds) {
-    if (band_cus) *band_cus = g_tune.band_cus;
-    if (interior_rounds) *interior_rounds = g_tune.rounds_multi;
-    return SMI_SUCCESS;
-}
-
-int smi_stencil_set_band_fusion(int fused, int balance_rows, int reserve_waves) {
-    SMI_ARG_CHECK(fused <= 1 && balance_rows <= 1024 && reserve_waves <= 65536,
-                  "fused / balance_rows / reserve_waves out of range");
-    if (fused >= 0) g_tune.band_fused = fused;
-    if (balance_rows >= 0) g_tune.band_balance = balance_rows;
-    if (reserve_waves >= 0) g_tune.band_reserve = reserve_waves;
-    return SMI_SUCCESS;
-}
-
-int smi_stencil_get_band_fusion(int *fused, int *balance_rows, int *reserve_waves) {
-    if (fused) *fused = g_tune.band_fused;
-    if (balance_rows) *balance_rows = g_tune.band_balance;
+int smi_stencil_get_bands(int *reserve_waves, int *interior_rounds) {
     if (reserve_waves) *reserve_waves = g_tune.band_reserve;
+    if (interior_rounds) *interior_rounds = g_tune.rounds_multi;
     return SMI_SUCCESS;
 }
 
@@ -338,7 +322,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     SMI_ARG_CHECK(px >= 1 && py >= 1 && px * py == c->size, "px*py must equal the communicator size");
     SMI_ARG_CHECK(timesteps >= 0, "timesteps < 0");
     SMI_ARG_CHECK(result_index, "NULL result_index");
-    hipStream_t s = (hipStream_t)stream_;  // main stream: the caller's, or the CU-masked one
+    hipStream_t s = (hipStream_t)stream_;
     hipStream_t cs = c->comm_stream;
     const int rows = x_local, cols = y_local;
     Neighbours nb = neighbours_of(c->rank, px, py);
@@ -495,22 +479,6 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     // the first phase the reference's artificial timestep t=0,
     // stencil_smi.cl:26-29,183-224).
     const bool overlap = g_tune.overlap != 0;
-    // CU partition (smi_stencil_set_bands): the band kernels and the exchange
-    // on band_cus reserved CUs, the interior on the rest in one round of
-    // waves; the caller's stream hands over to the pair and takes it back
-    const hipStream_t caller = s;
-    int reserve_waves = 0;
-    // fused passes: wave slots the interior leaves free for the exchange's
-    // kernels (smi_stencil_set_band_fusion)
-    const int reserve_fused = g_tune.band_reserve;
-    if (g_tune.band_cus > 0) {
-        int total = 0;
-        SMI_TRY(comm_cu_streams(c, g_tune.band_cus, &s, &cs, &total));
-        reserve_waves = std::max(1, resident_waves_of(plan.k[0] >= SWEEPK_MIN ? plan.k[0] : SWEEPK_MAX) *
-                                        g_tune.band_cus / total);
-        SMI_HIP_CHECK(hipEventRecord(ev_int, caller));
-        SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_int, 0));
-    }
     auto phase_start = [&]() -> int {
         SMI_HIP_CHECK(hipEventRecord(ev_int, s));
         SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
@@ -567,45 +535,11 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             };
             SMI_TRY(launch_packk(bufp(cur), rows, cols, K, hkv, cs));
             SMI_TRY(xchgk(bufp(cur), cs));
-            if (g_tune.band_fused && g_tune.band_cus == 0) {
-                // Fused passes: one launch per pass on the main stream (the
-                // interior sweep, whose band-carrying waves count their
-                // segments in a device counter); the comm stream waits on the
-                // counter, not on the launch, so the exchange of pass t runs
-                // beside the rest of its sweep, and pass t+1 waits for it:
-                //   comm : [counter >= segments(0..t)] exchange(t) -> rec E_x(t)
-                //   main : [wait E_x(t-1)] fused(t)
-                unsigned *done = nullptr;
-                SMI_TRY(comm_band_counter(c, &done));
-                SMI_HIP_CHECK(hipStreamWriteValue32(cs, done, 0u, 0));
-                SMI_TRY(plan_bands(K, &bk));
-                unsigned expect = 0;
-                for (int p = 0; p < npass; ++p, cur ^= 1) {
-                    bk.in = ak.in = bufp(cur);
-                    bk.out = ak.out = bufp(cur ^ 1);
-                    SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-                    SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-                    int segs = 0;
-                    SMI_TRY(launch_sweepk_fused(K, ak, bk, g_tune.band_balance, overlap ? reserve_fused : 0, done,
-                                                &segs, s));
-                    expect += (unsigned)segs;
-                    if (p == npass - 1) break;
-                    if (overlap) {
-                        SMI_HIP_CHECK(hipStreamWaitValue32(cs, done, expect, hipStreamWaitValueGte, 0xFFFFFFFFu));
-                    } else {
-                        SMI_HIP_CHECK(hipEventRecord(ev_int, s));
-                        SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
-                    }
-                    SMI_TRY(xchgk(ak.out, cs));
-                }
-                cur ^= 1;  // the loop's break skipped the last flip
-                continue;
-            }
             for (int p = 0; p < npass; ++p, cur ^= 1) {
                 bk.in = ak.in = bufp(cur);
                 bk.out = ak.out = bufp(cur ^ 1);
                 SMI_TRY(pass([&](hipStream_t st) { return launch_bandk(K, bk, st); },
-                             [&](hipStream_t st) { return launch_sweepk_ex(K, ak, 0, reserve_waves, true, st); },
+                             [&](hipStream_t st) { return launch_sweepk_ex(K, ak, 0, g_tune.band_reserve, true, st); },
                              xchgk, p < npass - 1, ak.out));
             }
         } else if (K == 2) {
@@ -642,14 +576,9 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             }
         }
     }
-    // the caller's stream owns the result: join the comm stream (and the
-    // CU-masked main stream)
+    // the caller's stream owns the result: join the comm stream
     SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-    SMI_HIP_CHECK(hipStreamWaitEvent(caller, ev_edge, 0));
-    if (s != caller) {
-        SMI_HIP_CHECK(hipEventRecord(ev_int, s));
-        SMI_HIP_CHECK(hipStreamWaitEvent(caller, ev_int, 0));
-    }
+    SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
     return SMI_SUCCESS;
 }
 

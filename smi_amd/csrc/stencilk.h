@@ -153,10 +153,6 @@ struct SweepK {
     int row_bytes;
     bool copyL, copyR, gT, gB;
     float4 W[K][3];   // level 0..K-1, slot = input row index mod 3
-    // fused multi-rank passes: the band segment this wave walked before its
-    // block is counted here once its stores completed -- at the pre-loop
-    // drain, which waits for them anyway (stencil_bandk.h); null otherwise
-    unsigned *signal = nullptr;
 
     template <bool REV>
     __device__ __forceinline__ float4 ld(int t) const {
@@ -319,11 +315,6 @@ struct SweepK {
         // store round trip per iteration); with it every wait in the loop
         // targets a load or store issued >= 2 rows of work before.
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
-        if (signal) {  // wave-uniform
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(signal, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            signal = nullptr;
-        }
         for (int t = PRO; t < n_in; t += 2 * U) {
 #pragma unroll
             for (int u = 0; u < U; ++u) B[u] = ld<REV>(t + U + u);
@@ -364,32 +355,20 @@ struct SweepK {
     }
 };
 
-// Row block rb of a strip: [row_lo + b(rb), row_lo + b(rb + 1)) with
-// balanced heights, except that the `ns` blocks of band-carrying waves
-// (stencil_bandk.h, fused multi-rank passes) are `ds` rows shorter; `cnt` =
-// how many of blocks [0, rb) are such blocks.  b(nrb) = out_rows.
-__device__ __forceinline__ int sweepk_block_row(int out_rows, int nrb, int ns, int ds, int rb, int cnt) {
-    const long tot = (long)out_rows + (long)ns * ds;
-    return (int)((long)rb * tot / nrb) - ds * cnt;
-}
-
 // The interior task of one wave: row block rb of strip `strip`.
 template <int K>
-__device__ __forceinline__ void sweepk_task(const SweepKArgs &a, int strip, int rb, int nrb, int ns, int ds, int cnt,
-                                            int lane, unsigned *signal = nullptr) {
+__device__ __forceinline__ void sweepk_task(const SweepKArgs &a, int strip, int rb, int nrb, int lane) {
     using S = SweepK<K, 3>;
     constexpr int SW = 256 - 2 * S::KC;  // output columns per window
     S w;
-    w.signal = signal;
     w.in = a.in;
     w.out = a.out;
     w.rows = a.rows;
     w.cols = a.cols;
     // balanced row blocks: every block of a tall rectangle has >= ht/2 rows
     const int out_rows = a.row_hi - a.row_lo;
-    // this block is short iff its wave carries a band segment (signal set)
-    w.o0 = a.row_lo + sweepk_block_row(out_rows, nrb, ns, ds, rb, cnt);
-    w.o1 = a.row_lo + sweepk_block_row(out_rows, nrb, ns, ds, rb + 1, cnt + (signal && ds > 0 ? 1 : 0));
+    w.o0 = a.row_lo + (int)((long)rb * out_rows / nrb);
+    w.o1 = a.row_lo + (int)((long)(rb + 1) * out_rows / nrb);
     // strips start at whole 128-byte lines (col_lo rounded down to 32
     // columns): a multi-rank interior starts KC columns in, and windows
     // stored from there would straddle a line at both ends of every row
@@ -455,7 +434,7 @@ __global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, 
     const int strip = task - rb * nstrips;
 #endif
     if (rb >= nrb) return;  // wave-uniform
-    sweepk_task<K>(a, strip, rb, nrb, 0, 0, 0, lane);
+    sweepk_task<K>(a, strip, rb, nrb, lane);
 }
 
 template <int K>

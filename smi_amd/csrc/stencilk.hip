@@ -35,30 +35,14 @@ static int resident_waves(int K) {
     }
 }
 
-int resident_waves_of(int K) { return resident_waves(K); }
-
 int sweepk_window_cols(int K) { return 256 - 8 * sweepk_apron_lanes(K); }
 
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s) { return launch_sweepk_ex(K, a, 0, 0, true, s); }
 
-#define SMI_FUSED_DECL(K)                                                                                \
-    int sweepk_fused_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, const BandKArgs &b, int ds,  \
-                                 unsigned *done, int blocks, hipStream_t s);
-SMI_FUSED_DECL(3)
-SMI_FUSED_DECL(4)
-SMI_FUSED_DECL(5)
-SMI_FUSED_DECL(6)
-SMI_FUSED_DECL(7)
-SMI_FUSED_DECL(8)
-SMI_FUSED_DECL(9)
-SMI_FUSED_DECL(10)
-SMI_FUSED_DECL(11)
-SMI_FUSED_DECL(12)
-
 // Strips and row blocks of a K-step sweep over a's output rectangle.
 // ht > 0: rows per wave as given; else automatic (g_tune.htk, or one round
 // of resident waves -- minus `reserve` waves left to the comm stream's
-// kernels in a multi-rank run).
+// kernels in a multi-rank run, smi_stencil_set_bands).
 static void sweepk_geometry(int K, const SweepKArgs &a, int ht_req, int reserve, int *nstrips_, int *nrb_) {
     const int sw = sweepk_window_cols(K);
     const int nstrips = (a.col_hi - (a.col_lo & ~31) + sw - 1) / sw;  // line-aligned strips (stencilk.h)
@@ -126,49 +110,6 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
     case 10: rc = sweepk_launch_k10(a, nstrips, nrb, blocks, s); break;
     case 11: rc = sweepk_launch_k11(a, nstrips, nrb, blocks, s); break;
     default: rc = sweepk_launch_k12(a, nstrips, nrb, blocks, s); break;
-    }
-    SMI_TRY(rc);
-    if (tok >= 0) SMI_TRY(prof_end(tok, s));
-    return SMI_SUCCESS;
-}
-
-// A fused multi-rank pass (stencil_bandk.h, sweepk_fused_kernel): the
-// interior sweep of `a` whose waves also compute the band segments of `b`
-// (b planned by plan_bands), each counted in `done` when finished.
-// balance_rows: how many rows shorter the row blocks of the band-carrying
-// waves are (0: segments dealt to the first waves, no balancing).  Returns
-// the number of band segments (the counter's increment) in *segments.
-int launch_sweepk_fused(int K, const SweepKArgs &a, const BandKArgs &b, int balance_rows, int reserve,
-                        unsigned *done, int *segments, hipStream_t s) {
-    SMI_TRY(check_sweepk(K, a));
-    const int nb = b.first[4];
-    *segments = nb;
-    int nstrips = 1, nrb = 0;
-    if (a.row_hi > a.row_lo && a.col_hi > a.col_lo) sweepk_geometry(K, a, 0, reserve, &nstrips, &nrb);
-    const long tasks = (long)nstrips * nrb;
-    // balanced only while every strip has enough row blocks for its share
-    // of segments and the short blocks stay >= 2K rows
-    const int out_rows = a.row_hi - a.row_lo;
-    int ds = balance_rows;
-    if (nb > tasks || (nrb > 0 && out_rows / nrb - ds < 2 * K)) ds = 0;
-    const long waves = ds > 0 ? tasks : std::max<long>(tasks, nb);
-    const int blocks = (int)((waves + 3) / 4);
-    if (blocks == 0) return SMI_SUCCESS;
-    int tok = -1;
-    if (prof_enabled())
-        SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)a.rows * a.cols * K, true));
-    int rc = SMI_SUCCESS;
-    switch (K) {
-    case 3: rc = sweepk_fused_launch_k3(a, nstrips, nrb, b, ds, done, blocks, s); break;
-    case 4: rc = sweepk_fused_launch_k4(a, nstrips, nrb, b, ds, done, blocks, s); break;
-    case 5: rc = sweepk_fused_launch_k5(a, nstrips, nrb, b, ds, done, blocks, s); break;
-    case 6: rc = sweepk_fused_launch_k6(a, nstrips, nrb, b, ds, done, blocks, s); break;
-    case 7: rc = sweepk_fused_launch_k7(a, nstrips, nrb, b, ds, done, blocks, s); break;
-    case 8: rc = sweepk_fused_launch_k8(a, nstrips, nrb, b, ds, done, blocks, s); break;
-    case 9: rc = sweepk_fused_launch_k9(a, nstrips, nrb, b, ds, done, blocks, s); break;
-    case 10: rc = sweepk_fused_launch_k10(a, nstrips, nrb, b, ds, done, blocks, s); break;
-    case 11: rc = sweepk_fused_launch_k11(a, nstrips, nrb, b, ds, done, blocks, s); break;
-    default: rc = sweepk_fused_launch_k12(a, nstrips, nrb, b, ds, done, blocks, s); break;
     }
     SMI_TRY(rc);
     if (tok >= 0) SMI_TRY(prof_end(tok, s));

@@ -19,6 +19,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <type_traits>
 
 #include "smi_internal.h"
 
@@ -200,23 +201,57 @@ std::unique_ptr<Transport> make_rccl_transport(int rank, int size,
 // ================================================================ local ==
 namespace {
 
+// Events of the in-process transport come from a pool owned by the group, so
+// that an event recorded by one rank outlives that rank's transport while
+// another rank may still wait on it (a detached send's `done` is recorded by
+// the receiver and waited for by the sender when it finalizes).  A handle
+// returns its event to the pool when the last Post holding it is gone, i.e.
+// once every wait on it has been enqueued (a wait captures the event's
+// current record, so re-recording it afterwards is safe).
+struct EventPool {
+    std::mutex mu;
+    std::vector<hipEvent_t> free;
+    ~EventPool() {
+        for (auto e : free) (void)hipEventDestroy(e);
+    }
+};
+using Ev = std::shared_ptr<std::remove_pointer<hipEvent_t>::type>;
+
+int pooled_event(const std::shared_ptr<EventPool> &pool, Ev *out) {
+    hipEvent_t e = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(pool->mu);
+        if (!pool->free.empty()) {
+            e = pool->free.back();
+            pool->free.pop_back();
+        }
+    }
+    if (!e) SMI_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *out = Ev(e, [pool](hipEvent_t x) {
+        std::lock_guard<std::mutex> lk(pool->mu);
+        pool->free.push_back(x);
+    });
+    return SMI_SUCCESS;
+}
+
 struct Post {
     const void *buf = nullptr;
     size_t bytes = 0;
-    hipEvent_t ready = nullptr;  // sender's stream reached the send (one per sender group)
-    hipEvent_t done = nullptr;   // receiver's copy finished (recorded by the receiver)
+    Ev ready;                    // sender's stream reached the send (one per sender group)
+    Ev done;                     // receiver's copy finished (recorded by the receiver)
     bool copied = false;         // `done` has been recorded
     int status = SMI_SUCCESS;
 };
 
 struct LocalGroup {
+    std::shared_ptr<EventPool> events = std::make_shared<EventPool>();
     int size = 0;
     std::mutex mu;
     std::condition_variable cv;
     // (src, dst, space): space 0 = bulk groups, 1 = element-channel packets
     // (send_detached / recv_now), matched FIFO within each space only
     std::map<std::tuple<int, int, int>, std::deque<std::shared_ptr<Post>>> mailbox;
-    int joined = 0;
+    int joined = 0;  // transports created for it (its ranks)
     std::map<int, int> dups;  // k-th smi_comm_dup of this group -> its group id
 };
 
@@ -239,7 +274,19 @@ int local_group_size(int group_id) {
 
 class LocalTransport final : public Transport {
   public:
-    LocalTransport(std::shared_ptr<LocalGroup> g, int rank) : g_(std::move(g)), rank_(rank) {}
+    LocalTransport(std::shared_ptr<LocalGroup> g, int rank, int id) : g_(std::move(g)), rank_(rank), id_(id) {
+        std::lock_guard<std::mutex> lk(g_->mu);
+        ++g_->joined;
+    }
+    ~LocalTransport() override {
+        // The last rank of a fully joined group drops the registry's
+        // reference too, so the group -- and the events of its pool -- go
+        // with this transport (finalize, HIP alive), not at process exit.
+        std::lock_guard<std::mutex> lk(g_groups_mu);
+        auto it = g_groups.find(id_);
+        if (it != g_groups.end() && it->second == g_ && g_->joined == g_->size && g_.use_count() == 2)
+            g_groups.erase(it);
+    }
 
     // begin() .. end() hold the bulk mutex (see RcclTransport::begin)
     int begin(hipStream_t stream) override {
@@ -282,10 +329,10 @@ class LocalTransport final : public Transport {
     }
     int end_group() {
         std::vector<std::shared_ptr<Post>> mine;
-        hipEvent_t ready = nullptr;
+        Ev ready;
         if (!sends_.empty()) {
-            SMI_TRY(get_event(&ready));
-            SMI_HIP_CHECK(hipEventRecord(ready, stream_));
+            SMI_TRY(pooled_event(g_->events, &ready));
+            SMI_HIP_CHECK(hipEventRecord(ready.get(), stream_));
         }
         for (auto &sd : sends_) {
             auto p = std::make_shared<Post>();
@@ -324,13 +371,15 @@ class LocalTransport final : public Transport {
             std::vector<hipEvent_t> waited;
             int st = SMI_SUCCESS;
             for (auto &p : got)
-                if (p->status == SMI_SUCCESS && std::find(waited.begin(), waited.end(), p->ready) == waited.end()) {
-                    waited.push_back(p->ready);
-                    if (hipStreamWaitEvent(stream_, p->ready, 0) != hipSuccess) st = SMI_ERR_HIP;
+                if (p->status == SMI_SUCCESS &&
+                    std::find(waited.begin(), waited.end(), p->ready.get()) == waited.end()) {
+                    waited.push_back(p->ready.get());
+                    if (hipStreamWaitEvent(stream_, p->ready.get(), 0) != hipSuccess) st = SMI_ERR_HIP;
                 }
             if (st == SMI_SUCCESS) st = launch_copies(src.data(), dst.data(), by.data(), (int)src.size(), stream_);
-            hipEvent_t done = nullptr;
-            if (get_event(&done) != SMI_SUCCESS || hipEventRecord(done, stream_) != hipSuccess) st = SMI_ERR_HIP;
+            Ev done;
+            if (pooled_event(g_->events, &done) != SMI_SUCCESS || hipEventRecord(done.get(), stream_) != hipSuccess)
+                st = SMI_ERR_HIP;
             if (st != SMI_SUCCESS) {
                 set_error("local transport: HIP copy failed");
                 if (rc == SMI_SUCCESS) rc = st;
@@ -344,7 +393,6 @@ class LocalTransport final : public Transport {
                 }
             }
             g_->cv.notify_all();
-            if (done) SMI_TRY(retire(done));
         }
 
         std::vector<hipEvent_t> joined;
@@ -357,12 +405,11 @@ class LocalTransport final : public Transport {
                 set_error("local transport: peer failed to receive");
                 rc = p->status;
             }
-            if (p->done && std::find(joined.begin(), joined.end(), p->done) == joined.end()) {
-                joined.push_back(p->done);
-                SMI_HIP_CHECK(hipStreamWaitEvent(stream_, p->done, 0));
+            if (p->done && std::find(joined.begin(), joined.end(), p->done.get()) == joined.end()) {
+                joined.push_back(p->done.get());
+                SMI_HIP_CHECK(hipStreamWaitEvent(stream_, p->done.get(), 0));
             }
         }
-        if (ready) SMI_TRY(retire(ready));
         sends_.clear();
         recvs_.clear();
         return rc;
@@ -377,8 +424,8 @@ class LocalTransport final : public Transport {
         auto p = std::make_shared<Post>();
         p->buf = buf;
         p->bytes = bytes;
-        SMI_TRY(get_event(&p->ready));
-        SMI_HIP_CHECK(hipEventRecord(p->ready, stream));
+        SMI_TRY(pooled_event(g_->events, &p->ready));
+        SMI_HIP_CHECK(hipEventRecord(p->ready.get(), stream));
         {
             std::lock_guard<std::mutex> lk(g_->mu);
             g_->mailbox[{rank_, peer, 1}].push_back(p);
@@ -398,13 +445,13 @@ class LocalTransport final : public Transport {
         if (p->bytes != bytes) {
             set_error("local transport: send/recv size mismatch");
             st = SMI_ERR_COMM;
-        } else if (hipStreamWaitEvent(stream, p->ready, 0) != hipSuccess ||
+        } else if (hipStreamWaitEvent(stream, p->ready.get(), 0) != hipSuccess ||
                    (bytes && hipMemcpyAsync(buf, p->buf, bytes, hipMemcpyDeviceToDevice, stream) != hipSuccess)) {
             set_error("local transport: HIP copy failed");
             st = SMI_ERR_HIP;
         }
-        hipEvent_t done = nullptr;
-        if (get_event(&done) != SMI_SUCCESS || hipEventRecord(done, stream) != hipSuccess) {
+        Ev done;
+        if (pooled_event(g_->events, &done) != SMI_SUCCESS || hipEventRecord(done.get(), stream) != hipSuccess) {
             if (st == SMI_SUCCESS) st = SMI_ERR_HIP;
         }
         {
@@ -414,7 +461,6 @@ class LocalTransport final : public Transport {
             p->copied = true;
         }
         g_->cv.notify_all();
-        if (done) SMI_TRY(retire(done));
         return st;
     }
     int ticket_wait(SendTicket *t) override {
@@ -427,10 +473,8 @@ class LocalTransport final : public Transport {
         t->live = false;
         t->impl.reset();
         int st = p->status;
-        // `done` may since have been recycled and recorded again by the
-        // receiver: then this waits for that later work too (never less)
-        if (p->done) SMI_HIP_CHECK(hipEventSynchronize(p->done));
-        SMI_TRY(retire(p->ready));
+        // the Post holds `done`: it cannot have been recycled yet
+        if (p->done) SMI_HIP_CHECK(hipEventSynchronize(p->done.get()));
         if (st != SMI_SUCCESS) set_error("local transport: peer failed to receive");
         return st;
     }
@@ -438,40 +482,6 @@ class LocalTransport final : public Transport {
     // The k-th dup of every rank of a group lands in one new group (created
     // by whichever rank gets there first).
     std::unique_ptr<Transport> dup(int *rc) override;
-
-    ~LocalTransport() override {
-        // finalize has synchronised the device: no queue references them now
-        for (auto e : retired_) hipEventDestroy(e);
-        for (auto e : free_) hipEventDestroy(e);
-    }
-
-  private:
-    // Event pool.  An event may still be referenced by barrier packets that
-    // another rank's stream has not processed yet, so a retired event is
-    // reused only after a device-wide synchronisation (when many have piled
-    // up); fresh ones are created only until the pool is warm.
-    int get_event(hipEvent_t *e) {
-        std::lock_guard<std::mutex> lk(retire_mu_);
-        if (!free_.empty()) {
-            *e = free_.back();
-            free_.pop_back();
-            return SMI_SUCCESS;
-        }
-        SMI_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-        return SMI_SUCCESS;
-    }
-    int retire(hipEvent_t e) {
-        std::lock_guard<std::mutex> lk(retire_mu_);
-        retired_.push_back(e);
-        if (retired_.size() >= 4096) {
-            SMI_HIP_CHECK(hipDeviceSynchronize());
-            free_.insert(free_.end(), retired_.begin(), retired_.end());
-            retired_.clear();
-        }
-        return SMI_SUCCESS;
-    }
-    std::mutex retire_mu_;
-    std::vector<hipEvent_t> retired_, free_;
 
     // the next post from `peer` in `space` (FIFO per (src, dst, space))
     std::shared_ptr<Post> next_post(int peer, int space) {
@@ -490,6 +500,7 @@ class LocalTransport final : public Transport {
     };
     std::shared_ptr<LocalGroup> g_;
     int rank_;
+    int id_;
     int ndup_ = 0;
     std::mutex bulk_mu_;
     hipStream_t stream_ = nullptr;
@@ -529,7 +540,7 @@ std::unique_ptr<Transport> make_local_transport(int group_id, int rank, int *rc)
         return nullptr;
     }
     *rc = SMI_SUCCESS;
-    return std::make_unique<LocalTransport>(g, rank);
+    return std::make_unique<LocalTransport>(g, rank, group_id);
 }
 
 }  // namespace smi

@@ -116,34 +116,18 @@ def get_tuning() -> dict:
                 overlap=v[3].value)
 
 
-def set_bands(band_cus: int = -1, interior_rounds: int = -1) -> None:
-    """Multi-rank K-step scheduling (bit-neutral): CUs reserved for the band
-    kernel and the exchange (0 = they share the GPU with the interior sweep)
-    and rounds of resident waves the interior sweep is cut into when they
-    share it.  -1 keeps a setting."""
-    _lib.call("smi_stencil_set_bands", band_cus, interior_rounds)
+def set_bands(reserve_waves: int = -1, interior_rounds: int = -1) -> None:
+    """Multi-rank K-step scheduling (bit-neutral): wave slots the interior
+    sweep leaves free for the band kernel and the exchange (0 = none) and
+    rounds of resident waves the interior sweep is cut into.  -1 keeps a
+    setting."""
+    _lib.call("smi_stencil_set_bands", reserve_waves, interior_rounds)
 
 
 def get_bands() -> dict:
     v = [ctypes.c_int() for _ in range(2)]
     _lib.call("smi_stencil_get_bands", *[ctypes.byref(x) for x in v])
-    return dict(band_cus=v[0].value, interior_rounds=v[1].value)
-
-
-def set_band_fusion(fused: int = -1, balance_rows: int = -1, reserve_waves: int = -1) -> None:
-    """Multi-rank K-step passes (bit-neutral): fused = 1 runs the band
-    segments inside the interior sweep's launch and releases the exchange from
-    a device counter mid-pass (0: separate band kernel); balance_rows = how
-    much shorter the row blocks of band-carrying waves are; reserve_waves =
-    wave slots the sweep leaves free for the exchange (0: interior_rounds
-    rounds).  -1 keeps a setting."""
-    _lib.call("smi_stencil_set_band_fusion", fused, balance_rows, reserve_waves)
-
-
-def get_band_fusion() -> dict:
-    v = [ctypes.c_int() for _ in range(3)]
-    _lib.call("smi_stencil_get_band_fusion", *[ctypes.byref(x) for x in v])
-    return dict(fused=v[0].value, balance_rows=v[1].value, reserve_waves=v[2].value)
+    return dict(reserve_waves=v[0].value, interior_rounds=v[1].value)
 
 
 def set_fusion(steps_per_pass: int = 0, rows_per_wave: int = 0, rows_in_flight: int = 0) -> None:

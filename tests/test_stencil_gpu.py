@@ -350,50 +350,28 @@ def test_deep_decomposed(gpu, oracle_mod, k, pxpy, overlap):
 
 
 @pytest.mark.parametrize("k", [3, 7, 10, 12])
-@pytest.mark.parametrize("bands", [(0, 1), (0, 3), (8, 1), (16, 2), (24, 1), (64, 1)])
+@pytest.mark.parametrize("bands", [(0, 1), (0, 3), (64, 1), (500, 2), (65536, 1)])
 def test_band_tuning_is_bit_neutral(gpu, oracle_mod, k, bands):
-    """CUs reserved for the bands and the exchange (a CU-masked stream pair,
-    or none) and the interior's rounds of resident waves change scheduling
-    only: a 3x3 decomposition (one interior rank with all eight neighbours)
-    stays bit-exact, with and without overlap.  K = 7 and 10 have column
-    bands (KC = 8, 12) wider than K."""
+    """Wave slots the interior leaves to the band kernel and the exchange
+    (none .. more than the GPU holds) and the interior's rounds of resident
+    waves change scheduling only: a 3x3 decomposition (one interior rank with
+    all eight neighbours) and the 2x4 of the 8-GPU run stay bit-exact, with
+    and without overlap.  K = 7 and 10 have column bands (KC = 8, 12) wider
+    than K."""
     from smi_amd import stencil
-    band_cus, rounds = bands
+    reserve, rounds = bands
     old = stencil.get_bands()
-    stencil.set_bands(band_cus, rounds)
+    stencil.set_bands(reserve, rounds)
     try:
-        g = oracle_mod.init_uniform(3 * 61, 3 * 140, seed=k + band_cus)
-        for T in (k, 2 * k + 1):
-            for overlap in (1, 0):
-                got = _run_fused(g, T, 3, 3, overlap, k=k)
-                assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, bands, T, overlap)
-        assert stencil.get_bands() == dict(band_cus=band_cus, interior_rounds=rounds)
-    finally:
-        stencil.set_bands(old["band_cus"], old["interior_rounds"])
-
-
-@pytest.mark.parametrize("k", [3, 8, 12])
-@pytest.mark.parametrize("fusion", [(0, 0, 0), (1, 0, 0), (1, 12, 0), (1, 40, 0), (1, 12, 64), (1, 0, 500)])
-def test_band_fusion_is_bit_neutral(gpu, oracle_mod, k, fusion):
-    """Bands as a separate kernel, or fused into the interior sweep's launch
-    with the exchange released by the device counter: unbalanced, balanced
-    (row blocks of band-carrying waves 12 / 40 rows shorter -- 40 falls back
-    to unbalanced on short blocks), one round minus reserved wave slots.  A
-    3x3 decomposition (an interior rank) with and without overlap and the
-    2x4 of the driver's 8-GPU run stay bit-exact."""
-    from smi_amd import stencil
-    old = stencil.get_band_fusion()
-    stencil.set_band_fusion(*fusion)
-    try:
-        assert stencil.get_band_fusion() == dict(fused=fusion[0], balance_rows=fusion[1], reserve_waves=fusion[2])
-        for PX, PY, X, Y in ((3, 3, 3 * 301, 3 * 700), (2, 4, 2 * 96, 4 * 128)):
-            g = oracle_mod.init_uniform(X, Y, seed=k + fusion[1] + PX)
-            for T in (2 * k, 2 * k + 1):
+        assert stencil.get_bands() == dict(reserve_waves=reserve, interior_rounds=rounds)
+        for PX, PY, X, Y in ((3, 3, 3 * 61, 3 * 140), (2, 4, 2 * 96, 4 * 128)):
+            g = oracle_mod.init_uniform(X, Y, seed=k + reserve % 97 + PX)
+            for T in (k, 2 * k + 1):
                 for overlap in (1, 0):
                     got = _run_fused(g, T, PX, PY, overlap, k=k)
-                    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, fusion, PX, PY, T, overlap)
+                    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, bands, PX, PY, T, overlap)
     finally:
-        stencil.set_band_fusion(old["fused"], old["balance_rows"], old["reserve_waves"])
+        stencil.set_bands(old["reserve_waves"], old["interior_rounds"])
 
 
 @pytest.mark.parametrize("k", [4, 8, 12])

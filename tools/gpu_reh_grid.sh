@@ -21,7 +21,7 @@ import glob, json
 for p in sorted(glob.glob("$O/rehearsal_*.jsonl")):
     for l in open(p):
         r = json.loads(l)
-        print(p.split("rehearsal_")[-1][:-6].ljust(14), r["exchange"][:9].ljust(9), "r", r["rounds"], "fusion", r.get("band_fusion"),
+        print(p.split("rehearsal_")[-1][:-6].ljust(14), r["exchange"][:9].ljust(9), "r", r["rounds"], "reserve", r.get("reserve_waves"),
               "ov", r["overlap"], "nob" if r.get("no_bands") else "   ", "loop %.2f alone %.2f eff %.4f" % (
               r["ms_per_step_interior_rank"] * 1e3, r["ms_per_step_alone"] * 1e3, r["efficiency"]))
 PY

@@ -12,10 +12,8 @@ are not the stencil's -- timing only.  Prints ms/step next to the plain
 single-tile run, i.e. an estimate of per-GPU weak-scaling efficiency with
 an exchange that costs one device-to-device copy of the halo bytes.
 REHEARSAL_ROUNDS (list) sets the rounds of resident waves the multi-rank
-interior sweep is cut into, REHEARSAL_BAND_CUS (list) the CUs reserved for the
-band kernel and the exchange (smi_stencil_set_bands; 0 = shared GPU).
-REHEARSAL_BANDFUSION (list of fused:balance_rows:reserve_waves, default
-1:12:0) the band placement (smi_stencil_set_band_fusion).
+interior sweep is cut into, REHEARSAL_RESERVE (list) the wave slots it leaves
+free for the band kernel and the exchange (smi_stencil_set_bands).
 REHEARSAL_PROF=0 times the runs without the library's profiling markers (the
 band / interior averages are then not reported).
 SMI_LOOPBACK_FUSED=1 prices the exchange as one copy kernel (like one RCCL
@@ -71,13 +69,9 @@ def main():
         alone = timed(comm, t, sc, steps)[0]
         noxchg = os.environ.get("SMI_LOOPBACK_NOXCHG")
         grid = [(r, b) for r in (int(x) for x in os.environ.get("REHEARSAL_ROUNDS", "1,2,3").split(","))
-                for b in (int(x) for x in os.environ.get("REHEARSAL_BAND_CUS", "0").split(","))]
-        fusions = [tuple(int(v) for v in f.split(":"))
-                   for f in os.environ.get("REHEARSAL_BANDFUSION", "1:12:0").split(",")]
-        grid = [(r, b, f) for r, b in grid for f in fusions]
-        for rounds, band_cus, fusion in grid:
-            stencil.set_bands(band_cus, rounds)
-            stencil.set_band_fusion(*fusion)
+                for b in (int(x) for x in os.environ.get("REHEARSAL_RESERVE", "0").split(","))]
+        for rounds, reserve in grid:
+            stencil.set_bands(reserve, rounds)
             for ov in [int(x) for x in os.environ.get("REHEARSAL_OVERLAP", "1,0").split(",")]:
                 stencil.set_tuning(overlap=ov)
                 # the lone tile right before each setting (the GPU clock
@@ -91,7 +85,7 @@ def main():
                 band = profiling.read(profiling.EDGE)
                 sweep = profiling.read(profiling.SWEEPK if k >= 4 else profiling.SWEEP)
                 os.environ.pop("SMI_LOOPBACK", None)
-                print(json.dumps({"K": k, "rounds": rounds, "band_cus": band_cus, "band_fusion": list(fusion), "no_bands": bool(os.environ.get("SMI_REH_NOBANDS")), "mask_layout": int(os.environ.get("SMI_REH_MASK_LAYOUT", "0")), "prof": os.environ.get("REHEARSAL_PROF", "1") != "0", "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
+                print(json.dumps({"K": k, "rounds": rounds, "reserve_waves": reserve, "no_bands": bool(os.environ.get("SMI_REH_NOBANDS")), "prof": os.environ.get("REHEARSAL_PROF", "1") != "0", "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
                                   "ms_per_step_alone": round(alone, 5),
                                   "ms_per_step_interior_rank": round(loop, 5),
                                   "efficiency": round(alone / loop, 4),
@@ -99,7 +93,7 @@ def main():
                                   "band_avg_ms": round(band[0] / max(band[1], 1), 5),
                                   "interior_avg_ms": round(sweep[0] / max(sweep[1], 1), 5)}), flush=True)
     stencil.set_tuning(overlap=1)
-    stencil.set_bands(0, 2)
+    stencil.set_bands(0, 1)
     comm.finalize()
 
 
