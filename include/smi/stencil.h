@@ -86,8 +86,10 @@ int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in
 
 /* Multi-rank K-step passes: the interior sweep runs beside the band kernel
  * (the halo-facing bands, on the comm stream) and the exchange.
- * reserve_waves = wave slots the interior sweep leaves free for them (0 =
- * none: the band kernel fills the interior's tail), interior_rounds =
+ * reserve_waves = wave slots the interior sweep leaves free for them, and
+ * the band kernel then runs as that many waves looping over its segments
+ * (0 = none reserved: one band wave per segment, run in the interior's
+ * tail), interior_rounds =
  * rounds of resident waves the interior sweep is cut into (default 1).  Pass
  * < 0 to keep.  Scheduling only: bit-identical results for every setting. */
 int smi_stencil_set_bands(int reserve_waves, int interior_rounds);

@@ -69,7 +69,10 @@ int comm_workspace(Comm *c, size_t bytes, void **ptr) {
 int comm_event(Comm *c, int idx, hipEvent_t *ev) {
     while ((int)c->events.size() <= idx) {
         hipEvent_t e;
-        SMI_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        // device-side ordering between this communicator's streams only: no
+        // system-scope release at the record (it made the kernel before it
+        // write its L2 back to memory, ~10 us between stencil passes)
+        SMI_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
         c->events.push_back(e);
     }
     *ev = c->events[idx];

@@ -237,18 +237,28 @@ __device__ __forceinline__ void bandk_wave(const BandKArgs &a, int wv, int lane)
     }
 }
 
-// the bands alone (beside the interior sweep on another stream); four
-// independent waves per workgroup
+// The bands beside the interior sweep (on the comm stream); four
+// independent waves per workgroup.  With one wave per segment (~800 at
+// 8192^2, K = 12) the kernel needs more wave slots than the interior's one
+// round leaves, and its waves only run in the interior's tail -- the exchange
+// then sits between two passes.  With fewer waves than segments (the wave
+// slots the interior reserves, smi_stencil_set_bands) every wave walks
+// segments wv, wv + waves, ... in turn and the bands finish beside the
+// interior, so the exchange overlaps it.
 template <int K>
 __global__ __launch_bounds__(256) void bandk_kernel(BandKArgs a) {
-    const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-    if (wv >= a.first[4]) return;  // wave-uniform
-    bandk_wave<K>(a, wv, threadIdx.x & 63);
+    const int waves = gridDim.x * 4;
+    const int wv0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+    for (int wv = wv0; wv < a.first[4]; wv += waves)  // wave-uniform
+        bandk_wave<K>(a, wv, threadIdx.x & 63);
 }
 
 template <int K>
-int bandk_launch_impl(const BandKArgs &a, int waves, hipStream_t s) {
-    hipLaunchKernelGGL((bandk_kernel<K>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+int bandk_launch_impl(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t stop) {
+    if (stop)  // completion event carried by the dispatch itself (no marker packet after it)
+        hipExtLaunchKernelGGL((bandk_kernel<K>), dim3((waves + 3) / 4), dim3(256), 0, s, nullptr, stop, 0, a);
+    else
+        hipLaunchKernelGGL((bandk_kernel<K>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
     SMI_HIP_CHECK(hipGetLastError());
     return SMI_SUCCESS;
 }
@@ -257,7 +267,7 @@ int bandk_launch_impl(const BandKArgs &a, int waves, hipStream_t s) {
 
 #define SMI_BANDK_INSTANCE(K)                                                                            \
     namespace smi {                                                                                      \
-    int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s) {                                \
-        return bandk_launch_impl<K>(a, waves, s);                                                        \
+    int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t stop) {               \
+        return bandk_launch_impl<K>(a, waves, s, stop);                                                  \
     }                                                                                                    \
     }

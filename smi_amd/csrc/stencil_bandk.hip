@@ -7,7 +7,7 @@
 
 namespace smi {
 
-#define SMI_BANDK_DECL(K) int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s);
+#define SMI_BANDK_DECL(K) int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t stop);
 SMI_BANDK_DECL(3)
 SMI_BANDK_DECL(4)
 SMI_BANDK_DECL(5)
@@ -45,24 +45,29 @@ int plan_bands(int K, BandKArgs *ap) {
     return SMI_SUCCESS;
 }
 
-int launch_bandk(int K, BandKArgs a, hipStream_t s) {
+int launch_bandk(int K, BandKArgs a, int max_waves, hipStream_t s, hipEvent_t stop) {
     SMI_TRY(plan_bands(K, &a));
-    const int n = a.first[4];
-    if (n == 0) return SMI_SUCCESS;
+    const int segs = a.first[4];
+    if (segs == 0) {
+        if (stop) SMI_HIP_CHECK(hipEventRecord(stop, s));
+        return SMI_SUCCESS;
+    }
+    // one wave per segment, or at most max_waves (> 0) waves looping over them
+    const int n = max_waves > 0 ? std::min(segs, std::max(4, max_waves)) : segs;
     int tok = -1;
     if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_EDGE, s, &tok, K));
     int rc = SMI_SUCCESS;
     switch (K) {
-    case 3: rc = bandk_launch_k3(a, n, s); break;
-    case 4: rc = bandk_launch_k4(a, n, s); break;
-    case 5: rc = bandk_launch_k5(a, n, s); break;
-    case 6: rc = bandk_launch_k6(a, n, s); break;
-    case 7: rc = bandk_launch_k7(a, n, s); break;
-    case 8: rc = bandk_launch_k8(a, n, s); break;
-    case 9: rc = bandk_launch_k9(a, n, s); break;
-    case 10: rc = bandk_launch_k10(a, n, s); break;
-    case 11: rc = bandk_launch_k11(a, n, s); break;
-    default: rc = bandk_launch_k12(a, n, s); break;
+    case 3: rc = bandk_launch_k3(a, n, s, stop); break;
+    case 4: rc = bandk_launch_k4(a, n, s, stop); break;
+    case 5: rc = bandk_launch_k5(a, n, s, stop); break;
+    case 6: rc = bandk_launch_k6(a, n, s, stop); break;
+    case 7: rc = bandk_launch_k7(a, n, s, stop); break;
+    case 8: rc = bandk_launch_k8(a, n, s, stop); break;
+    case 9: rc = bandk_launch_k9(a, n, s, stop); break;
+    case 10: rc = bandk_launch_k10(a, n, s, stop); break;
+    case 11: rc = bandk_launch_k11(a, n, s, stop); break;
+    default: rc = bandk_launch_k12(a, n, s, stop); break;
     }
     SMI_TRY(rc);
     if (tok >= 0) SMI_TRY(prof_end(tok, s));

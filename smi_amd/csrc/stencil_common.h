@@ -125,7 +125,8 @@ constexpr int SWEEPK_MIN = 3, SWEEPK_MAX = 12;
 // stores), else the minimal ceil(K / 4).
 __host__ __device__ constexpr int sweepk_apron_lanes(int K) { return K >= 9 ? 4 : (K + 3) / 4; }
 int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s);
-int launch_sweepk_ex(int K, const SweepKArgs &a, int ht, int reserve, bool prof, hipStream_t s);
+int launch_sweepk_ex(int K, const SweepKArgs &a, int ht, int reserve, bool prof, hipStream_t s,
+                     hipEvent_t stop = nullptr);
 int sweepk_window_cols(int K);  // output columns per 256-column window
 
 // Depth-K halos (stencil_bandk.h / stencil_bandk.hip).  KC = 4 ceil(K/4):
@@ -157,7 +158,9 @@ struct BandKArgs {
     int rlo, rhi;      // rows of the left/right bands
 };
 int plan_bands(int K, BandKArgs *a);  // fills kc, first[], sw, rlo, rhi
-int launch_bandk(int K, BandKArgs a, hipStream_t s);
+// the bands of a pass: one wave per segment, or max_waves (> 0) waves;
+// stop (nullable): an event the launch's dispatch records at completion
+int launch_bandk(int K, BandKArgs a, int max_waves, hipStream_t s, hipEvent_t stop = nullptr);
 int launch_packk(const float *in, int rows, int cols, int K, const HaloK &h, hipStream_t s);
 
 }  // namespace smi

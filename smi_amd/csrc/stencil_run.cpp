@@ -485,34 +485,29 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
         return SMI_SUCCESS;
     };
     // one pass of a phase: ring (comm stream) + interior (main stream)
-    auto pass = [&](auto ring, auto interior, auto xchg, bool need_xchg, const float *out) -> int {
+    // ring(st, stop) / interior(st, stop): stop (nullable) = an event the
+    // launch records by its own dispatch (K-step passes: no marker packets
+    // between kernels; ~4 us per pass, tools/streambench); the other phases'
+    // kernels ignore it and it is recorded after them here.
+    auto pass = [&](auto ring, auto interior, auto xchg, bool need_xchg, const float *out, bool carries) -> int {
         if (overlap) {
             // The interior is enqueued before the exchange: posting the
             // transport's sends/receives costs host time (RCCL group, or
             // event + copy per message in-process) that must not delay the
             // interior's launch -- the trace of an interior rank showed the
             // main stream idle ~100 us per pass behind the exchange calls.
-#ifdef SMI_LOOPBACK_REHEARSAL
-            if (getenv("SMI_INTERIOR_FIRST")) {  // experiment: enqueue the interior before the bands
-                SMI_TRY(interior(s));
-                SMI_TRY(ring(cs));
-                SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-            } else
-#endif
-            {
-                SMI_TRY(ring(cs));
-                SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-                SMI_TRY(interior(s));
-            }
-            SMI_HIP_CHECK(hipEventRecord(ev_int, s));
+            SMI_TRY(ring(cs, carries ? ev_edge : nullptr));
+            if (!carries) SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
+            SMI_TRY(interior(s, carries ? ev_int : nullptr));
+            if (!carries) SMI_HIP_CHECK(hipEventRecord(ev_int, s));
             SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
             if (need_xchg) SMI_TRY(xchg(out, cs));
             SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
         } else {
             SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
             SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
-            SMI_TRY(ring(s));
-            SMI_TRY(interior(s));
+            SMI_TRY(ring(s, nullptr));
+            SMI_TRY(interior(s, nullptr));
             SMI_HIP_CHECK(hipEventRecord(ev_int, s));
             SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
             if (need_xchg) SMI_TRY(xchg(out, cs));
@@ -538,9 +533,13 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             for (int p = 0; p < npass; ++p, cur ^= 1) {
                 bk.in = ak.in = bufp(cur);
                 bk.out = ak.out = bufp(cur ^ 1);
-                SMI_TRY(pass([&](hipStream_t st) { return launch_bandk(K, bk, st); },
-                             [&](hipStream_t st) { return launch_sweepk_ex(K, ak, 0, g_tune.band_reserve, true, st); },
-                             xchgk, p < npass - 1, ak.out));
+                SMI_TRY(pass([&](hipStream_t st, hipEvent_t stop) {
+                                 return launch_bandk(K, bk, g_tune.band_reserve, st, stop);
+                             },
+                             [&](hipStream_t st, hipEvent_t stop) {
+                                 return launch_sweepk_ex(K, ak, 0, g_tune.band_reserve, true, st, stop);
+                             },
+                             xchgk, p < npass - 1, ak.out, true));
             }
         } else if (K == 2) {
             // ---- pairs of steps (depth-2 halos)
@@ -549,8 +548,9 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             for (int p = 0; p < npass; ++p, cur ^= 1) {
                 a2.in = bufp(cur);
                 a2.out = bufp(cur ^ 1);
-                SMI_TRY(pass([&](hipStream_t st) { return launch_ring2(a2, h2, st); },
-                             [&](hipStream_t st) { return launch_sweep2(a2, st); }, xchg2, p < npass - 1, a2.out));
+                SMI_TRY(pass([&](hipStream_t st, hipEvent_t) { return launch_ring2(a2, h2, st); },
+                             [&](hipStream_t st, hipEvent_t) { return launch_sweep2(a2, st); }, xchg2, p < npass - 1,
+                             a2.out, false));
             }
         } else {
             // ---- single steps (depth-1 halos)
@@ -564,14 +564,14 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
                 a.in = inner.in = bufp(cur);
                 a.out = inner.out = bufp(cur ^ 1);
                 if (overlap) {
-                    SMI_TRY(pass([&](hipStream_t st) { return launch_edge(a, side_mask, st); },
-                                 [&](hipStream_t st) { return launch_sweep(inner, st); }, xchg1, t < npass - 1,
-                                 a.out));
+                    SMI_TRY(pass([&](hipStream_t st, hipEvent_t) { return launch_edge(a, side_mask, st); },
+                                 [&](hipStream_t st, hipEvent_t) { return launch_sweep(inner, st); }, xchg1,
+                                 t < npass - 1, a.out, false));
                 } else {
                     // the full sweep reads the halos itself
-                    SMI_TRY(pass([&](hipStream_t) { return (int)SMI_SUCCESS; },
-                                 [&](hipStream_t st) { return launch_sweep(a, st); }, xchg1, t < npass - 1,
-                                 a.out));
+                    SMI_TRY(pass([&](hipStream_t, hipEvent_t) { return (int)SMI_SUCCESS; },
+                                 [&](hipStream_t st, hipEvent_t) { return launch_sweep(a, st); }, xchg1,
+                                 t < npass - 1, a.out, false));
                 }
             }
         }

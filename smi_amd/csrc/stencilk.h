@@ -63,6 +63,8 @@
 
 #include <type_traits>
 
+#include <hip/hip_ext.h>
+
 #include "stencil_common.h"
 
 #ifndef SMI_SWEEPK_SCALED
@@ -438,8 +440,11 @@ __global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, 
 }
 
 template <int K>
-int sweepk_launch_impl(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s) {
-    hipLaunchKernelGGL((sweepk_kernel<K>), dim3(blocks), dim3(256), 0, s, a, nstrips, nrb);
+int sweepk_launch_impl(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s, hipEvent_t stop) {
+    if (stop)  // completion event carried by the dispatch itself (no marker packet after it)
+        hipExtLaunchKernelGGL((sweepk_kernel<K>), dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, a, nstrips, nrb);
+    else
+        hipLaunchKernelGGL((sweepk_kernel<K>), dim3(blocks), dim3(256), 0, s, a, nstrips, nrb);
     SMI_HIP_CHECK(hipGetLastError());
     return SMI_SUCCESS;
 }
@@ -464,8 +469,9 @@ int sweepk_resident_impl() {
 // compile in parallel.
 #define SMI_SWEEPK_INSTANCE(K)                                                                           \
     namespace smi {                                                                                      \
-    int sweepk_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s) {       \
-        return sweepk_launch_impl<K>(a, nstrips, nrb, blocks, s);                                        \
+    int sweepk_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s,         \
+                           hipEvent_t stop) {                                                            \
+        return sweepk_launch_impl<K>(a, nstrips, nrb, blocks, s, stop);                                  \
     }                                                                                                    \
     int sweepk_resident_k##K() { return sweepk_resident_impl<K>(); }                                     \
     }

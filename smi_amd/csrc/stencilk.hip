@@ -7,7 +7,8 @@
 namespace smi {
 
 #define SMI_SWEEPK_DECL(K)                                                                           \
-    int sweepk_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s);        \
+    int sweepk_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s,         \
+                           hipEvent_t stop);                                                             \
     int sweepk_resident_k##K();
 SMI_SWEEPK_DECL(3)
 SMI_SWEEPK_DECL(4)
@@ -55,11 +56,6 @@ static void sweepk_geometry(int K, const SweepKArgs &a, int ht_req, int reserve,
         // into several rounds so that workgroups retire during the pass and
         // the comm stream's kernels are dispatched then.
         int waves = resident_waves(K);
-#ifdef SMI_LOOPBACK_REHEARSAL
-        // experiment: leave a share of the wave slots to the band kernel
-        if (const char *e = getenv("SMI_INTERIOR_PCT"))
-            if (!(a.gT && a.gB && a.gL && a.gR)) waves = std::max(1, waves * atoi(e) / 100);
-#endif
         const bool single = a.gT && a.gB && a.gL && a.gR;
         int rounds = single ? 1 : std::max(1, g_tune.rounds_multi);
         if (!single && reserve > 0) {
@@ -81,9 +77,15 @@ static int check_sweepk(int K, const SweepKArgs &a) {
     return SMI_SUCCESS;
 }
 
-// prof: record the launch under SMI_PROF_STENCIL_SWEEPK
-int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool prof, hipStream_t s) {
-    if (a.row_hi <= a.row_lo || a.col_hi <= a.col_lo) return SMI_SUCCESS;
+// prof: record the launch under SMI_PROF_STENCIL_SWEEPK.  stop (nullable):
+// an event the launch's dispatch records when the kernel completes (or an
+// ordinary record when there is nothing to launch).
+int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool prof, hipStream_t s,
+                     hipEvent_t stop) {
+    if (a.row_hi <= a.row_lo || a.col_hi <= a.col_lo) {
+        if (stop) SMI_HIP_CHECK(hipEventRecord(stop, s));
+        return SMI_SUCCESS;
+    }
     SMI_TRY(check_sweepk(K, a));
     int nstrips = 0, nrb = 0;
     sweepk_geometry(K, a, ht_req, reserve, &nstrips, &nrb);
@@ -100,16 +102,16 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
                            true));
     int rc = SMI_SUCCESS;
     switch (K) {
-    case 3: rc = sweepk_launch_k3(a, nstrips, nrb, blocks, s); break;
-    case 4: rc = sweepk_launch_k4(a, nstrips, nrb, blocks, s); break;
-    case 5: rc = sweepk_launch_k5(a, nstrips, nrb, blocks, s); break;
-    case 6: rc = sweepk_launch_k6(a, nstrips, nrb, blocks, s); break;
-    case 7: rc = sweepk_launch_k7(a, nstrips, nrb, blocks, s); break;
-    case 8: rc = sweepk_launch_k8(a, nstrips, nrb, blocks, s); break;
-    case 9: rc = sweepk_launch_k9(a, nstrips, nrb, blocks, s); break;
-    case 10: rc = sweepk_launch_k10(a, nstrips, nrb, blocks, s); break;
-    case 11: rc = sweepk_launch_k11(a, nstrips, nrb, blocks, s); break;
-    default: rc = sweepk_launch_k12(a, nstrips, nrb, blocks, s); break;
+    case 3: rc = sweepk_launch_k3(a, nstrips, nrb, blocks, s, stop); break;
+    case 4: rc = sweepk_launch_k4(a, nstrips, nrb, blocks, s, stop); break;
+    case 5: rc = sweepk_launch_k5(a, nstrips, nrb, blocks, s, stop); break;
+    case 6: rc = sweepk_launch_k6(a, nstrips, nrb, blocks, s, stop); break;
+    case 7: rc = sweepk_launch_k7(a, nstrips, nrb, blocks, s, stop); break;
+    case 8: rc = sweepk_launch_k8(a, nstrips, nrb, blocks, s, stop); break;
+    case 9: rc = sweepk_launch_k9(a, nstrips, nrb, blocks, s, stop); break;
+    case 10: rc = sweepk_launch_k10(a, nstrips, nrb, blocks, s, stop); break;
+    case 11: rc = sweepk_launch_k11(a, nstrips, nrb, blocks, s, stop); break;
+    default: rc = sweepk_launch_k12(a, nstrips, nrb, blocks, s, stop); break;
     }
     SMI_TRY(rc);
     if (tok >= 0) SMI_TRY(prof_end(tok, s));

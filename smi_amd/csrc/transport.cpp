@@ -226,7 +226,9 @@ int pooled_event(const std::shared_ptr<EventPool> &pool, Ev *out) {
             pool->free.pop_back();
         }
     }
-    if (!e) SMI_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // ordering between the ranks' streams on the device (no host reads device
+    // data behind them): no system-scope release at the record
+    if (!e) SMI_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
     *out = Ev(e, [pool](hipEvent_t x) {
         std::lock_guard<std::mutex> lk(pool->mu);
         pool->free.push_back(x);

@@ -41,12 +41,19 @@ struct Ctx {
     hipStream_t s, cs;
     hipEvent_t e_int, e_band;
     uint32_t *f_int, *f_band;  // hipMallocSignalMemory counters (mode 7)
+    static constexpr int kPool = 4096;
+    hipEvent_t pool[kPool];
 };
+constexpr int kPool = Ctx::kPool;
 
 static void big(Ctx &c, int p) {
     hipLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, c.s, p & 1 ? c.b : c.a, p & 1 ? c.a : c.b, c.n);
 }
 static void small(Ctx &c, hipStream_t st) { hipLaunchKernelGGL(small_kernel, dim3(800), dim3(64), 0, st, c.sink, 2000); }
+// a band stand-in that runs ~40 us: its completion must not gate the next big kernel
+static void small_long(Ctx &c, hipStream_t st) {
+    hipLaunchKernelGGL(small_kernel, dim3(16), dim3(64), 0, st, c.sink, 3000);
+}
 // the same launches with the completion event carried by the dispatch itself
 static void big_ev(Ctx &c, int p, hipEvent_t stop) {
     hipExtLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, c.s, nullptr, stop, 0, p & 1 ? c.b : c.a,
@@ -63,6 +70,11 @@ static void small_ev(Ctx &c, hipStream_t st, hipEvent_t stop) {
 // 4-6: the completion events carried by the kernel dispatches
 // (hipExtLaunchKernelGGL stop events), see run()
 // 7: as 2 with stream memory operations (write / wait value) for the joins
+// 8 / 9: as 2 with a ~40 us second-stream kernel, events re-recorded every
+// pass (8) or fresh per pass (9): does a wait see the record current when it
+// was enqueued, or a later one?
+// 10 / 11: as 2 / 8 with the main kernel's completion event carried by its
+// dispatch (hipExtLaunchKernelGGL) instead of a record packet
 static double run(Ctx &c, int mode, int passes) {
     CK(hipDeviceSynchronize());
     if (mode == 7) {  // counters restart at 0 (nothing pending on them now)
@@ -84,6 +96,29 @@ static double run(Ctx &c, int mode, int passes) {
             CK(hipEventRecord(c.e_int, c.s));
             CK(hipStreamWaitEvent(c.s, c.e_band, 0));
             CK(hipStreamWaitEvent(c.cs, c.e_int, 0));
+        } else if (mode == 10 || mode == 11) {
+            // 10: as 2, the main kernel's completion event carried by its
+            // dispatch (no record packet on the main stream); 11: the same
+            // with the long band stand-in
+            if (mode == 10) small(c, c.cs); else small_long(c, c.cs);
+            CK(hipEventRecord(c.e_band, c.cs));
+            big_ev(c, p, c.e_int);
+            CK(hipStreamWaitEvent(c.s, c.e_band, 0));
+            CK(hipStreamWaitEvent(c.cs, c.e_int, 0));
+        } else if (mode == 8 || mode == 9) {
+            // the stencil schedule with a long band stand-in; 8 re-records
+            // two events every pass, 9 takes fresh events for every pass
+            hipEvent_t eb = c.e_band, ei = c.e_int;
+            if (mode == 9) {
+                eb = c.pool[(2 * p) % kPool];
+                ei = c.pool[(2 * p + 1) % kPool];
+            }
+            small_long(c, c.cs);
+            CK(hipEventRecord(eb, c.cs));
+            big(c, p);
+            CK(hipEventRecord(ei, c.s));
+            CK(hipStreamWaitEvent(c.s, eb, 0));
+            CK(hipStreamWaitEvent(c.cs, ei, 0));
         } else if (mode == 7) {
             // as 2 with stream memory operations: monotone pass counters
             small(c, c.cs);
@@ -123,18 +158,19 @@ int main(int argc, char **argv) {
     CK(hipExtMallocWithFlags((void **)&c.f_int, 8, hipMallocSignalMemory));
     CK(hipExtMallocWithFlags((void **)&c.f_band, 8, hipMallocSignalMemory));
     printf("{\"can_use_stream_wait_value\": %d}\n", can_wait);
+    for (int i = 0; i < kPool; ++i) CK(hipEventCreateWithFlags(&c.pool[i], hipEventDisableTiming));
     int least, greatest;
     CK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     const char *evname[3] = {"default", "disable_timing", "disable_timing_sysfence"};
     const unsigned evflags[3] = {hipEventDefault, hipEventDisableTiming,
                                  hipEventDisableTiming | hipEventDisableSystemFence};
     for (int prio = 1; prio < 2; ++prio) {
-        for (int ef = 1; ef < 3; ++ef) {
+        for (int ef = 1; ef < 2; ++ef) {
             CK(hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking));
             CK(hipStreamCreateWithPriority(&c.cs, hipStreamNonBlocking, prio ? greatest : least));
             CK(hipEventCreateWithFlags(&c.e_int, evflags[ef]));
             CK(hipEventCreateWithFlags(&c.e_band, evflags[ef]));
-            for (int mode = 0; mode < 8; ++mode) {
+            for (int mode = 0; mode < 12; mode += (mode == 2 ? 6 : 1)) {
                 run(c, mode, 20);  // warm-up
                 const double us = run(c, mode, passes);
                 printf("{\"mode\": %d, \"comm_prio\": \"%s\", \"events\": \"%s\", \"us_per_pass\": %.2f}\n", mode,
