@@ -32,12 +32,18 @@ The JSON line also carries:
   roofline      -- the stencil kernel with the largest measured time in the
                    timed region (HIP events on the launch stream: one marker
                    between back-to-back passes, so each launch is timed from the
-                   end of the previous one) and every kernel's share of the region: algorithmic
-                   8 B/cell/step x cells x K per launch divided by its average
-                   duration, vs the 8 TB/s HBM3E peak -- above 1 because of
-                   temporal blocking; `traffic` is the HBM bytes per launch
-                   from the rocprofv3 PMC passes committed under profiles/ and
-                   `hbm_frac` = traffic / launch time / peak
+                   end of the previous one) and every kernel's share of the
+                   region.  achieved = the pass's compulsory bytes (every
+                   stored cell read once and written once, 8 B) / its average
+                   duration, frac = achieved / the 8 TB/s HBM3E peak;
+                   `traffic` = the HBM bytes per launch from the rocprofv3 PMC
+                   passes committed under profiles/ and hbm_frac = traffic /
+                   launch time / peak (over-fetch included); cell_step_GBs =
+                   8 B per cell-STEP x K steps per launch / launch time
+                   (temporal blocking, not a fraction of peak);
+                   kernel_avg_ms is cross-checked against the rocprofv3
+                   --kernel-trace --stats summary of the driver's own command
+                   (profiles/rocprof_driver_cmd.json)
   cpu_baseline  -- the oracle's C restatement of the reference stencil
                    (OpenMP, every thread of this job's CPU share) timed on
                    this host on a bounded sample (rank 0, N=1 only), with the
