@@ -149,6 +149,26 @@ int prof_begin(int kernel, hipStream_t stream, int *token, int tag, double units
     return SMI_SUCCESS;
 }
 
+// A record whose two events the caller hands to the launch itself
+// (hipExtLaunchKernelGGL start / stop events): the dispatch stamps the
+// kernel's own start and end, and no marker packet sits between kernels.
+int prof_launch(int kernel, int *token, int tag, double units, hipEvent_t *start, hipEvent_t *stop) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    ProfRec r;
+    r.kernel = kernel;
+    r.tag = tag;
+    r.units = units;
+    SMI_TRY(prof_get_event(&r.a));
+    SMI_TRY(prof_get_event(&r.b));
+    r.owns_a = true;
+    *start = r.a;
+    *stop = r.b;
+    *token = (int)g_prof_recs.size();
+    g_prof_recs.push_back(r);
+    g_prof_last = -1;  // nothing to chain to
+    return SMI_SUCCESS;
+}
+
 // the next prof_begin records its own marker (a caller's own work may
 // follow the last one on the stream)
 void prof_break_chain() {

@@ -140,6 +140,9 @@ bool prof_enabled();
 int prof_begin(int kernel, hipStream_t stream, int *token, int tag = 0, double units = 0.0, bool chain = false);
 int prof_end(int token, hipStream_t stream);
 void prof_break_chain();
+// A record timed by the launch's own dispatch: pass *start / *stop to
+// hipExtLaunchKernelGGL (no marker packets around the kernel).
+int prof_launch(int kernel, int *token, int tag, double units, hipEvent_t *start, hipEvent_t *stop);
 
 size_t type_size(int type);
 

@@ -254,9 +254,9 @@ __global__ __launch_bounds__(256) void bandk_kernel(BandKArgs a) {
 }
 
 template <int K>
-int bandk_launch_impl(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t stop) {
-    if (stop)  // completion event carried by the dispatch itself (no marker packet after it)
-        hipExtLaunchKernelGGL((bandk_kernel<K>), dim3((waves + 3) / 4), dim3(256), 0, s, nullptr, stop, 0, a);
+int bandk_launch_impl(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+    if (start || stop)  // events carried by the dispatch itself (no marker packets around it)
+        hipExtLaunchKernelGGL((bandk_kernel<K>), dim3((waves + 3) / 4), dim3(256), 0, s, start, stop, 0, a);
     else
         hipLaunchKernelGGL((bandk_kernel<K>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
     SMI_HIP_CHECK(hipGetLastError());
@@ -267,7 +267,8 @@ int bandk_launch_impl(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t s
 
 #define SMI_BANDK_INSTANCE(K)                                                                            \
     namespace smi {                                                                                      \
-    int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t stop) {               \
-        return bandk_launch_impl<K>(a, waves, s, stop);                                                  \
+    int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t start,                \
+                          hipEvent_t stop) {                                                             \
+        return bandk_launch_impl<K>(a, waves, s, start, stop);                                           \
     }                                                                                                    \
     }

@@ -7,7 +7,8 @@
 
 namespace smi {
 
-#define SMI_BANDK_DECL(K) int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t stop);
+#define SMI_BANDK_DECL(K) \
+    int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t start, hipEvent_t stop);
 SMI_BANDK_DECL(3)
 SMI_BANDK_DECL(4)
 SMI_BANDK_DECL(5)
@@ -54,23 +55,30 @@ int launch_bandk(int K, BandKArgs a, int max_waves, hipStream_t s, hipEvent_t st
     }
     // one wave per segment, or at most max_waves (> 0) waves looping over them
     const int n = max_waves > 0 ? std::min(segs, std::max(4, max_waves)) : segs;
+    // timed by the dispatch itself (as the K-step sweep, stencilk.hip); the
+    // caller's ordering event is then recorded right after the launch
+    hipEvent_t start = nullptr, kstop = stop, after = nullptr;
     int tok = -1;
-    if (prof_enabled()) SMI_TRY(prof_begin(SMI_PROF_STENCIL_EDGE, s, &tok, K));
+    if (prof_enabled()) {
+        SMI_TRY(prof_launch(SMI_PROF_STENCIL_EDGE, &tok, K, 0.0, &start, &kstop));
+        after = stop;
+    }
     int rc = SMI_SUCCESS;
     switch (K) {
-    case 3: rc = bandk_launch_k3(a, n, s, stop); break;
-    case 4: rc = bandk_launch_k4(a, n, s, stop); break;
-    case 5: rc = bandk_launch_k5(a, n, s, stop); break;
-    case 6: rc = bandk_launch_k6(a, n, s, stop); break;
-    case 7: rc = bandk_launch_k7(a, n, s, stop); break;
-    case 8: rc = bandk_launch_k8(a, n, s, stop); break;
-    case 9: rc = bandk_launch_k9(a, n, s, stop); break;
-    case 10: rc = bandk_launch_k10(a, n, s, stop); break;
-    case 11: rc = bandk_launch_k11(a, n, s, stop); break;
-    default: rc = bandk_launch_k12(a, n, s, stop); break;
+    case 3: rc = bandk_launch_k3(a, n, s, start, kstop); break;
+    case 4: rc = bandk_launch_k4(a, n, s, start, kstop); break;
+    case 5: rc = bandk_launch_k5(a, n, s, start, kstop); break;
+    case 6: rc = bandk_launch_k6(a, n, s, start, kstop); break;
+    case 7: rc = bandk_launch_k7(a, n, s, start, kstop); break;
+    case 8: rc = bandk_launch_k8(a, n, s, start, kstop); break;
+    case 9: rc = bandk_launch_k9(a, n, s, start, kstop); break;
+    case 10: rc = bandk_launch_k10(a, n, s, start, kstop); break;
+    case 11: rc = bandk_launch_k11(a, n, s, start, kstop); break;
+    default: rc = bandk_launch_k12(a, n, s, start, kstop); break;
     }
     SMI_TRY(rc);
-    if (tok >= 0) SMI_TRY(prof_end(tok, s));
+    if (after) SMI_HIP_CHECK(hipEventRecord(after, s));
+    (void)tok;
     return SMI_SUCCESS;
 }
 

@@ -422,8 +422,16 @@ __device__ __forceinline__ void sweepk_task(const SweepKArgs &a, int strip, int 
     }
 }
 
+// experiment switch (tools/sweepbench builds): waves per SIMD the register
+// allocation must allow (amdgpu_waves_per_eu); the library uses the default
+#ifdef SMI_SWEEPK_WPE
+#define SMI_SWEEPK_WPE_ATTR __attribute__((amdgpu_waves_per_eu(SMI_SWEEPK_WPE, SMI_SWEEPK_WPE)))
+#else
+#define SMI_SWEEPK_WPE_ATTR
+#endif
+
 template <int K>
-__global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, int nrb) {
+__global__ __launch_bounds__(256) SMI_SWEEPK_WPE_ATTR void sweepk_kernel(SweepKArgs a, int nstrips, int nrb) {
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
     const int task = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
@@ -440,9 +448,10 @@ __global__ __launch_bounds__(256) void sweepk_kernel(SweepKArgs a, int nstrips, 
 }
 
 template <int K>
-int sweepk_launch_impl(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s, hipEvent_t stop) {
-    if (stop)  // completion event carried by the dispatch itself (no marker packet after it)
-        hipExtLaunchKernelGGL((sweepk_kernel<K>), dim3(blocks), dim3(256), 0, s, nullptr, stop, 0, a, nstrips, nrb);
+int sweepk_launch_impl(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s, hipEvent_t start,
+                       hipEvent_t stop) {
+    if (start || stop)  // events carried by the dispatch itself (no marker packets around it)
+        hipExtLaunchKernelGGL((sweepk_kernel<K>), dim3(blocks), dim3(256), 0, s, start, stop, 0, a, nstrips, nrb);
     else
         hipLaunchKernelGGL((sweepk_kernel<K>), dim3(blocks), dim3(256), 0, s, a, nstrips, nrb);
     SMI_HIP_CHECK(hipGetLastError());
@@ -470,8 +479,8 @@ int sweepk_resident_impl() {
 #define SMI_SWEEPK_INSTANCE(K)                                                                           \
     namespace smi {                                                                                      \
     int sweepk_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s,         \
-                           hipEvent_t stop) {                                                            \
-        return sweepk_launch_impl<K>(a, nstrips, nrb, blocks, s, stop);                                  \
+                           hipEvent_t start, hipEvent_t stop) {                                          \
+        return sweepk_launch_impl<K>(a, nstrips, nrb, blocks, s, start, stop);                           \
     }                                                                                                    \
     int sweepk_resident_k##K() { return sweepk_resident_impl<K>(); }                                     \
     }

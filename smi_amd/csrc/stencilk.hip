@@ -8,7 +8,7 @@ namespace smi {
 
 #define SMI_SWEEPK_DECL(K)                                                                           \
     int sweepk_launch_k##K(const SweepKArgs &a, int nstrips, int nrb, int blocks, hipStream_t s,         \
-                           hipEvent_t stop);                                                             \
+                           hipEvent_t start, hipEvent_t stop);                                           \
     int sweepk_resident_k##K();
 SMI_SWEEPK_DECL(3)
 SMI_SWEEPK_DECL(4)
@@ -92,29 +92,33 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
     const int out_rows = a.row_hi - a.row_lo;
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
+    // Timed by the dispatch itself (start / stop events handed to the
+    // launch): the kernel's own duration, and no marker packet between two
+    // passes.  A caller's ordering event (`stop`, multi-rank passes) is then
+    // recorded right after the launch.
+    hipEvent_t start = nullptr, kstop = stop, after = nullptr;
     int tok = -1;
-    // chained markers: within one smi_stencil_run (which restarts the
-    // chain) back-to-back single-tile sweeps are timed from the end of the
-    // previous one (one marker per pass).  The chain holds only while nothing
-    // else was recorded in between (a multi-rank pass records on two streams).
-    if (prof && prof_enabled())
-        SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K,
-                           true));
+    if (prof && prof_enabled()) {
+        SMI_TRY(prof_launch(SMI_PROF_STENCIL_SWEEPK, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K, &start,
+                            &kstop));
+        after = stop;
+    }
     int rc = SMI_SUCCESS;
     switch (K) {
-    case 3: rc = sweepk_launch_k3(a, nstrips, nrb, blocks, s, stop); break;
-    case 4: rc = sweepk_launch_k4(a, nstrips, nrb, blocks, s, stop); break;
-    case 5: rc = sweepk_launch_k5(a, nstrips, nrb, blocks, s, stop); break;
-    case 6: rc = sweepk_launch_k6(a, nstrips, nrb, blocks, s, stop); break;
-    case 7: rc = sweepk_launch_k7(a, nstrips, nrb, blocks, s, stop); break;
-    case 8: rc = sweepk_launch_k8(a, nstrips, nrb, blocks, s, stop); break;
-    case 9: rc = sweepk_launch_k9(a, nstrips, nrb, blocks, s, stop); break;
-    case 10: rc = sweepk_launch_k10(a, nstrips, nrb, blocks, s, stop); break;
-    case 11: rc = sweepk_launch_k11(a, nstrips, nrb, blocks, s, stop); break;
-    default: rc = sweepk_launch_k12(a, nstrips, nrb, blocks, s, stop); break;
+    case 3: rc = sweepk_launch_k3(a, nstrips, nrb, blocks, s, start, kstop); break;
+    case 4: rc = sweepk_launch_k4(a, nstrips, nrb, blocks, s, start, kstop); break;
+    case 5: rc = sweepk_launch_k5(a, nstrips, nrb, blocks, s, start, kstop); break;
+    case 6: rc = sweepk_launch_k6(a, nstrips, nrb, blocks, s, start, kstop); break;
+    case 7: rc = sweepk_launch_k7(a, nstrips, nrb, blocks, s, start, kstop); break;
+    case 8: rc = sweepk_launch_k8(a, nstrips, nrb, blocks, s, start, kstop); break;
+    case 9: rc = sweepk_launch_k9(a, nstrips, nrb, blocks, s, start, kstop); break;
+    case 10: rc = sweepk_launch_k10(a, nstrips, nrb, blocks, s, start, kstop); break;
+    case 11: rc = sweepk_launch_k11(a, nstrips, nrb, blocks, s, start, kstop); break;
+    default: rc = sweepk_launch_k12(a, nstrips, nrb, blocks, s, start, kstop); break;
     }
     SMI_TRY(rc);
-    if (tok >= 0) SMI_TRY(prof_end(tok, s));
+    if (after) SMI_HIP_CHECK(hipEventRecord(after, s));
+    (void)tok;
     return SMI_SUCCESS;
 }
 

@@ -141,6 +141,30 @@ def test_fusion_setting_drives_the_plan():
         stencil.set_fusion(old["steps_per_pass"])
 
 
+def test_band_settings_roundtrip_and_validate():
+    """smi_stencil_set_bands: wave slots reserved for the band kernel + the
+    exchange and the interior's rounds; -1 keeps a setting, out-of-range
+    values are refused (host-only, no device needed)."""
+    from smi_amd import stencil
+    from smi_amd._lib import SMIError
+    old = stencil.get_bands()
+    assert old == dict(reserve_waves=0, interior_rounds=1)  # defaults (DESIGN.md §6)
+    try:
+        stencil.set_bands(128, 2)
+        assert stencil.get_bands() == dict(reserve_waves=128, interior_rounds=2)
+        stencil.set_bands(-1, 3)
+        assert stencil.get_bands() == dict(reserve_waves=128, interior_rounds=3)
+        stencil.set_bands(0, -1)
+        assert stencil.get_bands() == dict(reserve_waves=0, interior_rounds=3)
+        with pytest.raises(SMIError):
+            stencil.set_bands(65537, 1)
+        with pytest.raises(SMIError):
+            stencil.set_bands(0, 65)
+        assert stencil.get_bands() == dict(reserve_waves=0, interior_rounds=3)
+    finally:
+        stencil.set_bands(old["reserve_waves"], old["interior_rounds"])
+
+
 # ------------------------------------------------------ gloo, world_size 2 --
 def _free_port():
     s = socket.socket()

@@ -3,7 +3,8 @@
 # the driver's own command (--gpus 1 --steps 20 --warmup 5) and at its
 # defaults, rocprofv3 kernel stats of the driver's command and FETCH/WRITE
 # counter passes of the same command (its sweepk<10> passes), plus the same
-# for the default command's sweepk<12> and an SQ pass.  Afterwards, on the
+# for the default command's sweepk<12>, an SQ pass, and the interior-rank
+# rehearsal (one-kernel exchange and in-process transport) with a kernel trace.  Afterwards, on the
 # CPU: tools/pmc_summarize.py driver|pmc ... into profiles/ (see DESIGN.md §7).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -32,5 +33,8 @@ step pmc_fetch_k12 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-forma
 step pmc_write_k12 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/$O/pmc_w12 -o run -- python3 $R/bench.py --steps 48 --warmup 12 --no-cpu-baseline --no-aux > $R/$O/pmc_w12.log 2>&1
 step pmc_sq timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d $R/$O/sq -o run -- python3 $R/bench.py $DRV --no-cpu-baseline --no-aux > $R/$O/sq.log 2>&1
 cd $R
+G="REHEARSAL_PASSES=40 REHEARSAL_OVERLAP=1 REHEARSAL_ROUNDS=1 REHEARSAL_RESERVE=0"
+step rehearsal bash tools/gpu_reh_grid.sh $1/rehearsal "copy:$G SMI_LOOPBACK_FUSED=1" "transport:$G" "copy_b:$G SMI_LOOPBACK_FUSED=1" "transport_b:$G"
+step rehearsal_trace bash tools/gpu_trace_reh.sh $1/rehearsal "copy:$G SMI_LOOPBACK_FUSED=1"
 for f in bench_driver bench_default; do python -c "import json;d=json.load(open('$O/$f.json'));r=d['roofline'];print('$f',d['value'],d['ms_per_step'],r['frac'],r.get('hbm_frac'),r['kernel_avg_ms'],[(k['kernel'][:16],k['launches'],k['total_ms']) for k in r['kernels']])"; done
 echo ALLDONE
