@@ -30,10 +30,10 @@ runs the same number of them).
 
 The JSON line also carries:
   roofline      -- the stencil kernel with the largest measured time in the
-                   timed region (HIP events carried by each launch's own
-                   dispatch -- hipExtLaunchKernelGGL start / stop: the
-                   kernel's duration, no marker packets between passes) and
-                   every kernel's share of the
+                   timed region (HIP events on the launch stream: one marker
+                   between back-to-back single-tile passes, so each launch is
+                   timed from the end of the previous one; a multi-rank pass
+                   is timed by its own dispatch) and every kernel's share of the
                    region.  achieved = the pass's compulsory bytes (every
                    stored cell read once and written once, 8 B) / its average
                    duration, frac = achieved / the 8 TB/s HBM3E peak;

@@ -92,16 +92,26 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
     const int out_rows = a.row_hi - a.row_lo;
     const long tasks = (long)nstrips * nrb;
     const int blocks = (int)((tasks + 3) / 4);
-    // Timed by the dispatch itself (start / stop events handed to the
-    // launch): the kernel's own duration, and no marker packet between two
-    // passes.  A caller's ordering event (`stop`, multi-rank passes) is then
-    // recorded right after the launch.
+    // Timing (profiling on).  Back-to-back single-tile passes: one chained
+    // marker per pass (the end marker of pass i is the begin of pass i+1):
+    // the least host time per launch -- dispatch-carried start / stop events
+    // cost ~5 us more host time per launch, which a short timed run (the
+    // driver's 20 steps = 2 passes) sees (tools/exp/timed_overhead.py).  A
+    // multi-rank pass (`stop` given: the comm stream waits for the interior)
+    // is timed by its dispatch (start / stop handed to the launch; the
+    // caller's ordering event is recorded right after it).
     hipEvent_t start = nullptr, kstop = stop, after = nullptr;
     int tok = -1;
+    const double units = (double)out_rows * (a.col_hi - a.col_lo) * K;
+    bool marker = false;
     if (prof && prof_enabled()) {
-        SMI_TRY(prof_launch(SMI_PROF_STENCIL_SWEEPK, &tok, K, (double)out_rows * (a.col_hi - a.col_lo) * K, &start,
-                            &kstop));
-        after = stop;
+        if (stop) {
+            SMI_TRY(prof_launch(SMI_PROF_STENCIL_SWEEPK, &tok, K, units, &start, &kstop));
+            after = stop;
+        } else {
+            SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, units, true));
+            marker = true;
+        }
     }
     int rc = SMI_SUCCESS;
     switch (K) {
@@ -118,7 +128,7 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
     }
     SMI_TRY(rc);
     if (after) SMI_HIP_CHECK(hipEventRecord(after, s));
-    (void)tok;
+    if (marker) SMI_TRY(prof_end(tok, s));
     return SMI_SUCCESS;
 }
 
