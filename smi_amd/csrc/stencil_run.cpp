@@ -468,9 +468,10 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     auto xchg2 = [&](const float *tile, hipStream_t st) { return exchange2(c, nb, tile, rows, cols, hb, st); };
 
     // Schedule (two streams, no host synchronisation between passes):
-    //   comm stream : [wait interior(t-1)] ring(t) -> rec E_edge(t) -> exchange(t)
+    //   comm stream : [wait interior(t-1)] band(t) -> rec E_edge(t) -> exchange(t)
     //   main stream : [wait E_edge(t-1)] interior(t)    -> rec E_int(t)
-    // The ring kernel reads in(t) (interior cells from interior(t-1),
+    // The band kernel (the depth-K bands; the depth-2 / depth-1 phases use
+    // their ring / edge kernels) reads in(t) (interior cells from interior(t-1),
     // halo-facing cells from its own predecessor) and the halos of
     // exchange(t-1); the interior reads only in(t), never a halo vector, so
     // neither the halo-facing cells nor the xGMI exchange sit on its path.
@@ -484,7 +485,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
         SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
         return SMI_SUCCESS;
     };
-    // one pass of a phase: ring (comm stream) + interior (main stream)
+    // one pass of a phase: bands (comm stream) + interior (main stream)
     // ring(st, stop) / interior(st, stop): stop (nullable) = an event the
     // launch records by its own dispatch (K-step passes: no marker packets
     // between kernels; ~4 us per pass, tools/streambench); the other phases'
