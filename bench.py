@@ -591,6 +591,27 @@ def aux_collectives(comm, world: int, rank: int, stream, barrier) -> list:
     return out
 
 
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without initialising HIP: the
+    visibility variables when set, else the GPU nodes of the KFD topology."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() not in ("", "-1")])
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(base):
+            try:
+                with open(os.path.join(base, node, "gpu_id")) as f:
+                    n += int(f.read().strip() or 0) != 0
+            except (OSError, ValueError):
+                pass
+    except OSError:
+        return 0
+    return n
+
+
 def launch_ranks(args, argv: list[str]) -> int:
     """Start `args.gpus` ranks of this script as child processes (never an
     exec: the parent has not touched the GPU and does not), forward rank 0's
@@ -603,10 +624,10 @@ def launch_ranks(args, argv: list[str]) -> int:
     n = args.gpus
     fake = args.fake_host
     if not fake:
-        import torch  # device_count() does not initialise the GPU on this image
-        if torch.cuda.device_count() < n:
+        ngpu = visible_gpus()  # without HIP: the parent never touches the GPU
+        if ngpu < n:
             fake = True
-            sys.stderr.write(f"[bench] {torch.cuda.device_count()} GPU(s) visible for {n} ranks: --fake-host\n")
+            sys.stderr.write(f"[bench] {ngpu} GPU(s) visible for {n} ranks: --fake-host\n")
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
@@ -624,14 +645,26 @@ def launch_ranks(args, argv: list[str]) -> int:
                                       start_new_session=True))
     deadline = time.monotonic() + args.launch_timeout
     rc = 0
-    out0 = b""
-    try:
-        out0, _ = procs[0].communicate(timeout=max(1.0, deadline - time.monotonic()))
-        for p in procs:
-            p.wait(timeout=max(1.0, deadline - time.monotonic()))
-    except subprocess.TimeoutExpired:
-        sys.stderr.write(f"[bench] ranks outlived --launch-timeout {args.launch_timeout:.0f} s: killed\n")
-        rc = 124
+    # rank 0's line is read on a thread (a full pipe must never block it);
+    # the children are polled together: the first one to fail takes the
+    # others down at once (survivors would sit in RCCL until the deadline)
+    out = {}
+    reader = threading.Thread(target=lambda: out.setdefault("0", procs[0].stdout.read()), daemon=True)
+    reader.start()
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = next((c for c in codes if c not in (None, 0)), None)
+        if bad is not None:
+            sys.stderr.write(f"[bench] a rank exited with {bad}: stopping the others\n")
+            rc = bad
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > deadline:
+            sys.stderr.write(f"[bench] ranks outlived --launch-timeout {args.launch_timeout:.0f} s: killed\n")
+            rc = 124
+            break
+        time.sleep(0.2)
     for p in procs:  # each child leads its own process group (start_new_session)
         if p.poll() is None:
             try:
@@ -641,6 +674,8 @@ def launch_ranks(args, argv: list[str]) -> int:
             p.wait()
     if rc == 0:
         rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    reader.join(timeout=10)
+    out0 = out.get("0") or b""
     line = next((ln for ln in out0.decode(errors="replace").splitlines() if ln.startswith("{")), None)
     if line:
         sys.stdout.write(line + "\n")

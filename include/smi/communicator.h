@@ -69,11 +69,12 @@ int smi_get_unique_id(void *id, int id_bytes);
 int smi_init(int rank, int size, int device, const void *unique_id, int id_bytes,
              SMI_Comm *comm);
 
-/* In-process group: `size` ranks are host threads of this process (all on
- * `device` or on devices of their own).  smi_local_group_create returns a
+/* In-process group: `size` ranks are host threads of this process, all on
+ * one device (the first rank's `device`; smi_init_local returns
+ * SMI_ERR_INVALID_ARG for any other).  smi_local_group_create returns a
  * group id; each rank thread then calls smi_init_local with it.  Transfers
- * are device-to-device copies ordered by HIP events -- a GPU transport used
- * to run multi-rank parity tests on a single GPU. */
+ * are device-side copies ordered by HIP events -- a GPU transport used to run
+ * multi-rank parity tests on a single GPU. */
 int smi_local_group_create(int size, int *group_id);
 int smi_init_local(int group_id, int rank, int device, SMI_Comm *comm);
 

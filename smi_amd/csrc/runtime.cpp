@@ -239,7 +239,7 @@ int smi_init_local(int group_id, int rank, int device, SMI_Comm *comm) {
     SMI_ARG_CHECK(device >= 0 && device < ndev, "device out of range");
     SMI_HIP_CHECK(hipSetDevice(device));
     int rc = SMI_SUCCESS;
-    auto t = make_local_transport(group_id, rank, &rc);
+    auto t = make_local_transport(group_id, rank, device, &rc);
     if (rc != SMI_SUCCESS) return rc;
     auto c = std::make_unique<Comm>();
     c->rank = rank;

@@ -104,7 +104,8 @@ class Group {
 std::unique_ptr<Transport> make_rccl_transport(int rank, int size,
                                                const void *unique_id,
                                                int id_bytes, int *rc);
-std::unique_ptr<Transport> make_local_transport(int group_id, int rank,
+// device: the rank's device; every rank of a group must use the same one
+std::unique_ptr<Transport> make_local_transport(int group_id, int rank, int device,
                                                 int *rc);
 int local_group_size(int group_id);
 

@@ -334,7 +334,11 @@ __device__ __forceinline__ void sweepd_task(const SweepKArgs &a, int strip, int 
     w.r_begin = rev ? w.o1 - 1 + K : w.o0 - K;
     // column-edge strips run one variant for either side (the other side's
     // mask is empty): four walks per K instead of eight keep the build short
+#ifdef SMI_DEEP_FORCE  // experiment: every wave runs variant SMI_DEEP_FORCE (timing only, wrong results)
+    switch (SMI_DEEP_FORCE) {
+#else
     switch ((rev ? 2 : 0) + (ce ? 1 : 0)) {
+#endif
     case 0: w.template go<false, 0>(); break;
 #ifndef SMI_DEEP_INTERIOR_ONLY
     case 1: w.template go<false, 3>(); break;

@@ -6,10 +6,12 @@
 // transfer is a plain RCCL send/recv between the two ranks.
 //
 //  * RcclTransport  -- production: one process per GPU, RCCL over xGMI.
-//  * LocalTransport -- ranks are host threads of one process sharing one (or
-//    several) devices; a transfer is a device-to-device hipMemcpyAsync
-//    ordered by HIP events.  It exists so that multi-rank parity tests can run
-//    on a single GPU (RCCL refuses two ranks on one device).
+//  * LocalTransport -- ranks are host threads of one process sharing one
+//    device; a group's transfers are one copy kernel that reads the sender's
+//    buffer directly, ordered by HIP events without a system-scope fence
+//    (both valid only on one device: smi_init_local refuses a second one).
+//    It exists so that multi-rank parity tests can run on a single GPU (RCCL
+//    refuses two ranks on one device).
 #include <rccl/rccl.h>
 
 #include <condition_variable>
@@ -146,7 +148,10 @@ class RcclTransport final : public Transport {
     // Both communicators split again (color 0, same rank order): RCCL
     // matches the new pair's operations separately from this pair's.
     std::unique_ptr<Transport> dup(int *rc) override {
-        std::lock_guard<std::mutex> lk(bulk_mu_);
+        // chan_ carries the element channels (send_detached / recv_now take
+        // chan_mu_ from any host thread): no channel traffic may run on it
+        // while it is split, so both locks are held
+        std::scoped_lock lk(bulk_mu_, chan_mu_);
         ncclComm_t c2 = nullptr, ch2 = nullptr;
         *rc = check(ncclCommSplit(comm_, 0, rank_, &c2, nullptr), "ncclCommSplit");
         if (*rc != SMI_SUCCESS) return nullptr;
@@ -253,7 +258,9 @@ struct LocalGroup {
     // (src, dst, space): space 0 = bulk groups, 1 = element-channel packets
     // (send_detached / recv_now), matched FIFO within each space only
     std::map<std::tuple<int, int, int>, std::deque<std::shared_ptr<Post>>> mailbox;
-    int joined = 0;  // transports created for it (its ranks)
+    int device = -1;  // the one device every rank of the group runs on
+    int joined = 0;   // transports created for it (its ranks)
+    int live = 0;     // transports not yet destroyed
     std::map<int, int> dups;  // k-th smi_comm_dup of this group -> its group id
 };
 
@@ -279,15 +286,26 @@ class LocalTransport final : public Transport {
     LocalTransport(std::shared_ptr<LocalGroup> g, int rank, int id) : g_(std::move(g)), rank_(rank), id_(id) {
         std::lock_guard<std::mutex> lk(g_->mu);
         ++g_->joined;
+        ++g_->live;
     }
     ~LocalTransport() override {
-        // The last rank of a fully joined group drops the registry's
-        // reference too, so the group -- and the events of its pool -- go
-        // with this transport (finalize, HIP alive), not at process exit.
-        std::lock_guard<std::mutex> lk(g_groups_mu);
-        auto it = g_groups.find(id_);
-        if (it != g_groups.end() && it->second == g_ && g_->joined == g_->size && g_.use_count() == 2)
-            g_groups.erase(it);
+        // The rank whose transport goes last in a fully joined group drops
+        // the registry's reference too, so the group -- and the events of its
+        // pool -- go with this transport (finalize, HIP alive), not at
+        // process exit.  Counted under the group's mutex: ranks finalizing on
+        // their threads at the same time see distinct counts.  (g_->mu is
+        // released before g_groups_mu is taken: dup() nests them the other
+        // way round.)
+        bool last = false;
+        {
+            std::lock_guard<std::mutex> lk(g_->mu);
+            last = --g_->live == 0 && g_->joined >= g_->size;
+        }
+        if (last) {
+            std::lock_guard<std::mutex> lk(g_groups_mu);
+            auto it = g_groups.find(id_);
+            if (it != g_groups.end() && it->second == g_) g_groups.erase(it);
+        }
     }
 
     // begin() .. end() hold the bulk mutex (see RcclTransport::begin)
@@ -526,10 +544,15 @@ std::unique_ptr<Transport> LocalTransport::dup(int *rc) {
             g_->dups[k] = id;
         }
     }
-    return make_local_transport(id, rank_, rc);
+    int dev = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_->mu);
+        dev = g_->device;
+    }
+    return make_local_transport(id, rank_, dev, rc);
 }
 
-std::unique_ptr<Transport> make_local_transport(int group_id, int rank, int *rc) {
+std::unique_ptr<Transport> make_local_transport(int group_id, int rank, int device, int *rc) {
     auto g = find_group(group_id);
     if (!g) {
         set_error("unknown local group");
@@ -540,6 +563,17 @@ std::unique_ptr<Transport> make_local_transport(int group_id, int rank, int *rc)
         set_error("rank out of range for local group");
         *rc = SMI_ERR_INVALID_ARG;
         return nullptr;
+    }
+    {
+        // one device per group: the copy kernel reads the sender's buffer
+        // and the ordering events skip the system-scope fence
+        std::lock_guard<std::mutex> lk(g->mu);
+        if (g->device < 0) g->device = device;
+        if (g->device != device) {
+            set_error("in-process group: every rank must use the group's device (" + std::to_string(g->device) + ")");
+            *rc = SMI_ERR_INVALID_ARG;
+            return nullptr;
+        }
     }
     *rc = SMI_SUCCESS;
     return std::make_unique<LocalTransport>(g, rank, group_id);

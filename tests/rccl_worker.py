@@ -221,6 +221,40 @@ def dup_cases(comm, rank, world, s):
     d.finalize()
 
 
+def finalize_cases(comm, rank, world, s):
+    """The event-lifetime rule behind round 3's crash (a finalizing rank
+    destroyed an event its peer still waited on; fixed in 1074c45), made
+    deterministic: rank 0 posts detached element sends on a dup and calls
+    finalize at once (finalize drains: it returns when the peer has received
+    them); rank 1 waits until rank 0 is inside finalize, pops every element,
+    waits until rank 0's finalize has returned, then uses its own streams
+    again and finalizes."""
+    from torch.distributed import distributed_c10d as c10d
+    store = c10d._get_default_store()
+    d = comm.dup()
+    n = 1000
+    if rank == 0:
+        c = channels.open_send_channel(n, 1, 1, 3, d)
+        for i in range(n):
+            c.push(7 * i + 1)
+        store.set("fin/r0_entering", "1")
+        d.finalize()
+        store.set("fin/r0_done", "1")
+    elif rank == 1:
+        store.wait(["fin/r0_entering"])
+        time.sleep(0.05)
+        c = channels.open_receive_channel(n, 1, 0, 3, d)
+        got = [c.pop() for _ in range(n)]
+        store.wait(["fin/r0_done"])
+        x = torch.arange(1 << 16, device="cuda", dtype=torch.float32) * 3
+        torch.cuda.synchronize()
+        report(rank, "finalize with detached sends in flight",
+               got == [7 * i + 1 for i in range(n)] and float(x[-1]) == 3 * ((1 << 16) - 1))
+        d.finalize()
+    else:
+        d.finalize()
+
+
 def main():
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -231,7 +265,7 @@ def main():
     s = torch.cuda.Stream()
     try:
         with torch.cuda.stream(s):
-            for part in (bulk_cases, stencil_cases, channel_cases, dup_cases):
+            for part in (bulk_cases, stencil_cases, channel_cases, dup_cases, finalize_cases):
                 part(comm, rank, world, s)
                 s.synchronize()
                 dist.barrier()

@@ -379,3 +379,90 @@ def test_bulk_p2p_errors(gpu):
     with pytest.raises(SMIError):
         collectives.recv(comm, buf, 3)      # peer out of range
     comm.finalize()
+
+
+def test_finalize_with_detached_sends_in_flight(gpu):
+    """Round 3's crash (gpurun_out/r03_full1/gpu_tests.log: ranks finalizing
+    while peers were still inside element bcasts; the in-process transport
+    destroyed a `done` event a peer still waited on -- fixed in 1074c45 with
+    pool-owned event handles), made deterministic: rank 0 posts detached
+    element sends and calls finalize at once (finalize drains, i.e. returns
+    once the peer has received them); rank 1 waits until rank 0 is inside
+    finalize, pops every element, waits until rank 0's finalize has
+    returned and then keeps exchanging with rank 2 over the same group, whose
+    event pool must outlive rank 0's transport."""
+    import threading
+    import time
+    from smi_amd import LocalGroup, channels as ch
+    g = LocalGroup(3)
+    n = 1000
+    entering, done = threading.Event(), threading.Event()
+    res = {}
+    errs = []
+
+    def r0():
+        torch.cuda.set_device(0)
+        c = g.comm(0)
+        s = ch.open_send_channel(n, INT, 1, 3, c)
+        for i in range(n):
+            s.push(7 * i + 1)
+        entering.set()
+        c.finalize()
+        done.set()
+
+    def r1():
+        torch.cuda.set_device(0)
+        c = g.comm(1)
+        assert entering.wait(60)
+        time.sleep(0.05)
+        r = ch.open_receive_channel(n, INT, 0, 3, c)
+        res["from0"] = [r.pop() for _ in range(n)]
+        assert done.wait(60)
+        s = ch.open_send_channel(n, INT, 2, 4, c)
+        for i in range(n):
+            s.push(5 * i)
+        c.finalize()
+
+    def r2():
+        torch.cuda.set_device(0)
+        c = g.comm(2)
+        assert done.wait(60)
+        r = ch.open_receive_channel(n, INT, 1, 4, c)
+        res["from1"] = [r.pop() for _ in range(n)]
+        c.finalize()
+
+    def wrap(f):
+        def run():
+            try:
+                f()
+            except BaseException as e:  # noqa: BLE001
+                errs.append(e)
+        return run
+
+    ts = [threading.Thread(target=wrap(f), daemon=True) for f in (r0, r1, r2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+        assert not t.is_alive(), "rank thread hung"
+    assert not errs, errs
+    assert res["from0"] == [7 * i + 1 for i in range(n)]
+    assert res["from1"] == [5 * i for i in range(n)]
+
+
+def test_local_group_refuses_second_device(gpu):
+    """An in-process group runs on one device (its copy kernel reads the
+    sender's buffer, its ordering events skip the system-scope fence):
+    smi_init_local refuses a rank on another device."""
+    import ctypes
+    from smi_amd import LocalGroup, _lib
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (the check sits behind the device-range check)")
+    g = LocalGroup(2)
+    c0 = g.comm(0)
+    bad = _lib.SMI_Comm()
+    rc = _lib.load().smi_init_local(g.group_id, 1, 1, ctypes.byref(bad))
+    assert rc != 0
+    c1 = g.comm(1)
+    c0.finalize()
+    c1.finalize()
