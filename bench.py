@@ -22,8 +22,10 @@ RCCL over xGMI, overlapped with the interior sweep.  Inputs are resident in
 HBM before the timed region; the timed region is exactly K steps bracketed by
 a barrier + device synchronize on both sides; the time is the max over ranks.
 
-A run of T steps is planned as ceil(T / 12) sweep passes of at most 12 steps,
-balanced to within one step when T % 12 >= 3 (e.g. 20 = 10 + 10; config.plan).  Before the timed
+A run of T steps is planned as ceil(T / 20) sweep passes of at most 20 steps
+(single tile; passes of more than 12 steps run the rotating-ring sweep,
+stencild.h; multi-rank runs use at most 12), balanced to within one step
+when T % 20 >= 3 (config.plan; the driver's 20 steps are one pass).  Before the timed
 region every kernel of that plan launches once and untimed runs of the same
 plan repeat for at least --warmup-ms (GPU clock settling; with N > 1 every rank
 runs the same number of them).
@@ -96,6 +98,8 @@ PARITY_BOUNDED_STEPS = 48      # longer runs: the first 48 steps of the same pas
 
 def kernel_label(kind: int, tag: int) -> str:
     from smi_amd import profiling
+    if kind == profiling.SWEEPK and tag > 12:
+        return f"sweepd_kernel<{tag}> (smi_amd/csrc/stencild.h, rotating-ring sweep, {tag} Jacobi steps per launch)"
     if kind == profiling.SWEEPK:
         return f"sweepk_kernel<{tag}> (smi_amd/csrc/stencilk.h, {tag} Jacobi steps per launch)"
     if kind == profiling.SWEEP and tag == 2:
@@ -946,7 +950,8 @@ def main() -> None:
         },
     }
     if dom:
-        rp = rocprof_avg(f"sweepk_kernel<{spl}>") if dom["kind"] == profiling.SWEEPK else None
+        rp = (rocprof_avg(f"{'sweepd' if spl > 12 else 'sweepk'}_kernel<{spl}>")
+              if dom["kind"] == profiling.SWEEPK else None)
         if rp:
             rp["ratio_to_hip_events"] = round(rp["avg_ms"] / sweep_avg_ms, 4) if sweep_avg_ms else None
             out["roofline"]["rocprof"] = rp

@@ -67,12 +67,14 @@ int smi_stencil_set_tuning(int rows_per_wave, int rows_in_flight,
 int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
                            int *nontemporal_stores, int *overlap);
 
-/* Temporal blocking: steps_per_pass = K in 1..12 fuses up to K Jacobi steps
+/* Temporal blocking: steps_per_pass = K in 1..20 fuses up to K Jacobi steps
  * into one pass over HBM (same per-cell arithmetic, bit-identical result).
+ * K = 13..20 runs the rotating-ring sweep, on single tiles of at least 4K
+ * rows (shorter tiles and multi-rank runs clip K to 12).
  * Multi-rank runs then exchange depth-K halos -- K rows / KC = 4 ceil(K/4)
  * columns per side neighbour and a K x KC corner block per diagonal
  * neighbour -- once per K steps; a band kernel computes the halo-facing bands
- * (K rows / KC columns deep) while the interior sweep runs.  Default K = 12.  A run is planned as K-step passes;
+ * (K rows / KC columns deep) while the interior sweep runs.  A run is planned as K-step passes;
  * a remainder r = timesteps % K >= 3 is spread over ceil(timesteps / K)
  * passes balanced to within one step (20 = 10 + 10), r = 1 or 2 adds a pair
  * and/or a single step (smi_stencil_plan).  In a multi-rank run K is
@@ -94,6 +96,15 @@ int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in
  * < 0 to keep.  Scheduling only: bit-identical results for every setting. */
 int smi_stencil_set_bands(int reserve_waves, int interior_rounds);
 int smi_stencil_get_bands(int *reserve_waves, int *interior_rounds);
+
+/* The rotating-ring sweep (K = 13..20) launches one round of waves whose
+ * row blocks are shortened where a wave has more work per row: ce16 / rev16
+ * = the extra work of a wave holding a global-edge column / of the
+ * upward-walking bottom block, in 16ths of a plain wave's; waves = the
+ * launch's waves (0 = every resident wave slot).  Pass < 0 to keep.
+ * Scheduling only: bit-identical results for every setting. */
+int smi_stencil_set_deep(int ce16, int rev16, int waves);
+int smi_stencil_get_deep(int *ce16, int *rev16, int *waves);
 
 /* One phase of a planned run: `passes` launches of `steps_per_pass` steps. */
 typedef struct {

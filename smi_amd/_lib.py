@@ -65,6 +65,8 @@ SIGNATURES = {
     "smi_stencil_get_fusion": (I, [ctypes.POINTER(I)] * 3),
     "smi_stencil_set_bands": (I, [I, I]),
     "smi_stencil_get_bands": (I, [ctypes.POINTER(I)] * 2),
+    "smi_stencil_set_deep": (I, [I, I, I]),
+    "smi_stencil_get_deep": (I, [ctypes.POINTER(I)] * 3),
     "smi_reduce": (I, [SMI_Comm, P, P, SZ, I, I, I, I, P]),
     "smi_reduce_fold": (I, [P, P, I, SZ, SZ, I, I, P]),
     "smi_bcast": (I, [SMI_Comm, P, SZ, I, I, I, P]),

@@ -46,6 +46,13 @@ VARIANT_FLAGS = {
 }
 
 
+# Sources no variant switch reaches (no SMI_LOOPBACK* / SMI_BOUNDS_CHECK /
+# SMI_EXPERIMENTS in them or in what they include): every variant links the
+# release objects of these instead of compiling them again (the rotating-ring
+# sweep's eight instantiation units take minutes each).
+SHARED_PREFIXES = ("stencild_k",)
+
+
 def file_flags(src: str) -> list[str]:
     name = os.path.basename(src)
     return [f for prefix, fl in FILE_FLAGS.items() if name.startswith(prefix) for f in fl]
@@ -117,7 +124,14 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
             f.write(flags_txt)
     objs = []
     procs = []
+    if variant:
+        shared = [src for src in sources() if os.path.basename(src).startswith(SHARED_PREFIXES)]
+        if shared:
+            build(force=force, verbose=verbose)  # the release objects they come from
     for src in sources():
+        if variant and os.path.basename(src).startswith(SHARED_PREFIXES):
+            objs.append(os.path.join(OUT_DIR, os.path.basename(src) + ".o"))
+            continue
         obj = os.path.join(out_dir, os.path.basename(src) + ".o")
         objs.append(obj)
         if not force and not _obj_stale(src, obj, flags_file):

@@ -65,7 +65,7 @@ struct Tuning {
     int u = 16;         // rows in flight per batch
     int nt = 1;         // non-temporal stores
     int overlap = 1;    // overlap halo exchange with the interior sweep
-    int fuse = 12;      // Jacobi steps per pass over HBM (1..12; the remainder runs as one shallower pass)
+    int fuse = 20;      // Jacobi steps per pass over HBM (1..20; K > 12: rotating-ring sweep, single tiles)
     int ht2 = 8;        // rows per wave (two-step sweep)
     int u2 = 8;         // rows in flight per batch (two-step sweep)
     int htk = 0;        // rows per wave (K-step sweep, K >= 4); 0 = one round of resident waves
@@ -77,6 +77,13 @@ struct Tuning {
     int rounds_multi = 1;
     int band_reserve = 0;
     int uk = 3;        // rows loaded ahead (K-step sweep: one 3-row register batch, fixed at build time)
+    // deep sweep (stencild.hip): extra work of an edge-column strip's and of
+    // an upward-walking bottom block's waves, in 16ths of a plain block's
+    // (their blocks are shortened by it); waves of the launch (0 = one round
+    // of resident waves)
+    int deep_ce16 = 4;
+    int deep_rev16 = 2;
+    int deep_waves = 0;
 };
 extern Tuning g_tune;
 
@@ -128,6 +135,40 @@ int launch_sweepk(int K, const SweepKArgs &a, hipStream_t s);
 int launch_sweepk_ex(int K, const SweepKArgs &a, int ht, int reserve, bool prof, hipStream_t s,
                      hipEvent_t stop = nullptr);
 int sweepk_window_cols(int K);  // output columns per 256-column window
+
+// Deep K-step sweep (stencild.h / stencild.hip, SWEEPD_MIN <= K <= SWEEPD_MAX):
+// same arguments and output as the K-step sweep, for single-tile passes of
+// more than SWEEPK_MAX steps.  The launch geometry: strips of 256 - 2 KC
+// output columns; interior strips cut into nrb row blocks, the strips
+// holding a global-edge column (their waves run the per-lane column copy)
+// into nrb_ce shorter blocks, and in every strip the bottom block of a tile
+// with a global bottom edge (it walks upwards: one extra DPP move per W/E
+// pair) shortened to weight wlast/16 of a block -- so that every wave of the
+// single round finishes at about the same time.
+constexpr int SWEEPD_MIN = 13, SWEEPD_MAX = 20;
+struct SweepDGeom {
+    int nstrips;   // all strips
+    int n_int;     // interior strips (no global-edge column): [int0, int0 + n_int)
+    int int0;
+    int nrb;       // row blocks per interior strip
+    int ce[4];     // strip indices of the edge-column strips (-1: none)
+    int nrb_ce;    // row blocks per edge-column strip
+    int wlast;     // weight of a bottom block (gB) in 16ths of a block
+    int tasks;     // waves of the launch
+};
+// Rows [o0, o1) of block rb of nb in a strip: blocks of weight 16 except a
+// bottom block of weight wlast (integer arithmetic: both neighbours of a
+// boundary compute it identically).
+__host__ __device__ inline void sweepd_block_rows(const SweepKArgs &a, int rb, int nb, int wlast, int *o0, int *o1) {
+    const long out_rows = a.row_hi - a.row_lo;
+    const long den = (long)(nb - 1) * 16 + (a.gB ? wlast : 16);
+    *o0 = a.row_lo + (int)(out_rows * rb * 16 / den);
+    *o1 = rb == nb - 1 ? a.row_hi : a.row_lo + (int)(out_rows * (rb + 1) * 16 / den);
+}
+bool sweepd_fits(int K, const SweepKArgs &a);
+int sweepd_window_cols(int K);
+int sweepd_geometry(int K, const SweepKArgs &a, SweepDGeom *g);
+int launch_sweepd(int K, const SweepKArgs &a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
 
 // Depth-K halos (stencil_bandk.h / stencil_bandk.hip).  KC = 4 ceil(K/4):
 // the column depth, whole float4 groups.  Receive side: top = rows -K..-1 and

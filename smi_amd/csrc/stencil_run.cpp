@@ -217,9 +217,19 @@ static Plan make_plan(int rows, int cols, int timesteps, bool multi) {
     int K = fuse >= SWEEPK_MIN ? fuse : 0;
     if (K && multi) {
         // a multi-rank tile holds the K-row bands and the float4-aligned
-        // K-column bands (4 * ceil(K / 4) wide) of both sides
-        K = std::min(K, rows / 2);
+        // K-column bands (4 * ceil(K / 4) wide) of both sides; the band
+        // kernel and the depth-K halos go to SWEEPK_MAX
+        K = std::min({K, rows / 2, SWEEPK_MAX});
         while (K > 0 && 8 * ((K + 3) / 4) > cols) --K;
+    }
+    if (K > SWEEPK_MAX && !multi) {
+        // deep passes (stencild.h) need tall enough tiles: four blocks of K rows
+        SweepKArgs probe{};
+        probe.rows = rows;
+        probe.cols = cols;
+        probe.row_hi = rows;
+        probe.col_hi = cols;
+        if (!sweepd_fits(K, probe)) K = SWEEPK_MAX;
     }
     if (cols < 8 || K < SWEEPK_MIN) K = 0;
     int rest = timesteps;
@@ -250,7 +260,7 @@ extern "C" {
 
 int smi_stencil_set_fusion(int steps_per_pass, int rows_per_wave, int rows_in_flight) {
     if (steps_per_pass > 0) {
-        SMI_ARG_CHECK(steps_per_pass <= SWEEPK_MAX, "steps_per_pass must be 1..12");
+        SMI_ARG_CHECK(steps_per_pass <= SWEEPD_MAX, "steps_per_pass must be 1..20");
         g_tune.fuse = steps_per_pass;
     }
     // rows_per_wave / rows_in_flight tune the kernel of the current setting
@@ -285,6 +295,21 @@ int smi_stencil_set_bands(int reserve_waves, int interior_rounds) {
 int smi_stencil_get_bands(int *reserve_waves, int *interior_rounds) {
     if (reserve_waves) *reserve_waves = g_tune.band_reserve;
     if (interior_rounds) *interior_rounds = g_tune.rounds_multi;
+    return SMI_SUCCESS;
+}
+
+int smi_stencil_set_deep(int ce16, int rev16, int waves) {
+    SMI_ARG_CHECK(ce16 <= 256 && rev16 <= 256 && waves <= (1 << 20), "deep sweep settings out of range");
+    if (ce16 >= 0) g_tune.deep_ce16 = ce16;
+    if (rev16 >= 0) g_tune.deep_rev16 = rev16;
+    if (waves >= 0) g_tune.deep_waves = waves;
+    return SMI_SUCCESS;
+}
+
+int smi_stencil_get_deep(int *ce16, int *rev16, int *waves) {
+    if (ce16) *ce16 = g_tune.deep_ce16;
+    if (rev16) *rev16 = g_tune.deep_rev16;
+    if (waves) *waves = g_tune.deep_waves;
     return SMI_SUCCESS;
 }
 

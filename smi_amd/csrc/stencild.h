@@ -231,6 +231,54 @@ struct SweepD {
         if constexpr (TC < 0 || TC == 2 * K) store_row<REV, SC>(t, v);
     }
 
+    // Level l of the row at rotation J (TC as in row()): v = new_{l-1} in,
+    // new_l out.
+    template <bool REV, int CE, bool SC, int J, int TC, int l>
+    __device__ __forceinline__ void level(float4 &v) {
+        if constexpr (TC < 0 || TC >= 2 * l) {
+            constexpr int ia = ph(D + 2 * l, J), ib = ph(D + 2 * l - 1, J);  // A_{l-1}, B_{l-1}
+            const float4 older = R[ia], mid = R[ib];
+            float4 nv = step<REV, CE, SC>(older, mid, v);
+            if constexpr (TC >= 0 && TC - l == K) {
+                const float4 m = SC ? make_float4(mid.x * 4.0f, mid.y * 4.0f, mid.z * 4.0f, mid.w * 4.0f) : mid;
+                asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(nv.x) : "v"(m.x), "s"(maskE));
+                asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(nv.y) : "v"(m.y), "s"(maskE));
+                asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(nv.z) : "v"(m.z), "s"(maskE));
+                asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(nv.w) : "v"(m.w), "s"(maskE));
+            }
+            if constexpr (l < K) R[ia] = nv;
+            v = nv;
+        }
+    }
+
+    // Rows t and t + 1 (rotations J, J + 1), their level chains interleaved
+    // one level apart: row t + 1's level l - 1 needs row t's level l - 2
+    // only, so each pair of steps is independent -- twice the ILP of one
+    // chain, and the DPP / packed-result hazards of one chain are covered by
+    // the other's instructions instead of s_nop.  Row t + 1's load goes out
+    // after row t's level K (its register is row t's A_{K-1}).
+    template <bool REV, int CE, bool SC, int J, int TC>
+    __device__ __forceinline__ void pair(int t) {
+        constexpr int TB = TC < 0 ? -1 : TC + 1;
+        R[ph(0, J)] = ld<REV>(min(t + D, n_in - 1));
+        float4 va = R[ph(D, J)];
+        float4 vb = R[ph(D, J + 1)];
+        if constexpr (SC) {
+            note(va);
+            note(vb);
+        }
+        level<REV, CE, SC, J, TC, 1>(va);
+        static_for<K - 1>([&](auto L) {
+            constexpr int l = L + 2;
+            level<REV, CE, SC, J, TC, l>(va);
+            level<REV, CE, SC, J + 1, TB, l - 1>(vb);
+        });
+        if constexpr (TC < 0 || TC == 2 * K) store_row<REV, SC>(t, va);
+        R[ph(0, J + 1)] = ld<REV>(min(t + 1 + D, n_in - 1));
+        level<REV, CE, SC, J + 1, TB, K>(vb);
+        if constexpr (TB < 0 || TB == 2 * K) store_row<REV, SC>(t + 1, vb);
+    }
+
     // Rows t + r .. t + N - 1 of one loop body (a whole cycle: the rotation
     // is the same at both ends, no register is ever copied), as a chain of
     // nested checks: the walk's end leaves the loop at once (the ring is dead
@@ -243,11 +291,18 @@ struct SweepD {
             // the walk's end is checked every G rows: the rows of a group
             // schedule together (a row past the end loads the clamped last row
             // and stores nothing)
+#ifdef SMI_DEEP_PAIR
+            static_assert(N % 2 == 0, "pairs of rows need an even cycle (D odd)");
+            if (t + r >= n_in) return false;
+            pair<REV, CE, SC, (J0 + r) % N, -1>(t + r);
+            return body<REV, CE, SC, r + 2, J0>(t);
+#else
             if constexpr (r % G == 0) {
                 if (t + r >= n_in) return false;
             }
             row<REV, CE, SC, (J0 + r) % N, -1>(t + r);
             return body<REV, CE, SC, r + 1, J0>(t);
+#endif
         }
     }
 
@@ -266,6 +321,14 @@ struct SweepD {
             if (!body<REV, CE, SC, 0, 0>(t)) break;
 #else
         // prologue: input rows 0 .. 2K, compile-time t (rotation j = t)
+#ifdef SMI_DEEP_PAIR
+        row<REV, CE, SC, 0, 0>(0);
+        static_for<K>([&](auto P) {
+            constexpr int t = 2 * P + 1;
+            __builtin_amdgcn_sched_barrier(0);
+            pair<REV, CE, SC, t % N, t>(t);
+        });
+#else
         static_for<PRO>([&](auto T) {
             constexpr int t = T;
             // scheduling regions of G rows, as in the loop (one region of
@@ -273,6 +336,7 @@ struct SweepD {
             if constexpr (t % G == 0 && t > 0) __builtin_amdgcn_sched_barrier(0);
             row<REV, CE, SC, t % N, t>(t);
         });
+#endif
         // steady state: N rows per iteration from rotation PRO mod N
         for (int t = PRO;; t += N)
             if (!body<REV, CE, SC, 0, PRO % N>(t)) break;
@@ -296,12 +360,12 @@ struct SweepD {
     }
 };
 
-// Row blocks of the deep sweep: block 0 starts at row_lo, the last ends at
-// row_hi, every block has at least K rows (so only the first block of a
-// tile with gT reaches row 0, only the last with gB row X-1; the host
-// checks), balanced.
+// One wave: strip `strip`, block rb of nb.  The host guarantees that every
+// block has at least K rows and that a tile with both global row edges has
+// two blocks or more (so only the first block of a tile with gT reaches row
+// 0, only the last with gB row X-1).
 template <int K>
-__device__ __forceinline__ void sweepd_task(const SweepKArgs &a, int strip, int rb, int nrb, int lane) {
+__device__ __forceinline__ void sweepd_task(const SweepKArgs &a, int strip, int rb, int nb, int wlast, int lane) {
     using S = SweepD<K>;
     constexpr int SW = 256 - 2 * S::KC;
     S w;
@@ -309,9 +373,7 @@ __device__ __forceinline__ void sweepd_task(const SweepKArgs &a, int strip, int 
     w.out = a.out;
     w.rows = a.rows;
     w.cols = a.cols;
-    const int out_rows = a.row_hi - a.row_lo;
-    w.o0 = a.row_lo + (int)((long)rb * out_rows / nrb);
-    w.o1 = a.row_lo + (int)((long)(rb + 1) * out_rows / nrb);
+    sweepd_block_rows(a, rb, nb, wlast, &w.o0, &w.o1);
     w.n_in = (w.o1 - w.o0) + 2 * K;
     const int cs = (a.col_lo & ~31) + strip * SW;
     const int cb = cs - S::KC + 4 * lane;
@@ -354,16 +416,52 @@ __device__ __forceinline__ void sweepd_task(const SweepKArgs &a, int strip, int 
 #define SMI_DEEP_WPE 1
 #endif
 
+// Task order: the interior strips' blocks row band by row band (the waves of
+// a workgroup are neighbouring strips of one band: their overlapping window
+// columns meet in L2), then the edge-column strips' blocks.
 template <int K>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMI_DEEP_WPE, 8))) void sweepd_kernel(
-    SweepKArgs a, int nstrips, int nrb) {
+    SweepKArgs a, SweepDGeom g) {
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
     const int lane = threadIdx.x & 63;
     const int task = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
-    const int rb = task / nstrips;
-    const int strip = task - rb * nstrips;
-    if (rb >= nrb) return;  // wave-uniform
-    sweepd_task<K>(a, strip, rb, nrb, lane);
+    if (task >= g.tasks) return;  // wave-uniform
+    const int ti = g.n_int * g.nrb;
+    if (task < ti) {
+        const int rb = task / g.n_int;
+        sweepd_task<K>(a, g.int0 + task - rb * g.n_int, rb, g.nrb, g.wlast, lane);
+    } else {
+        const int t2 = task - ti;
+        const int k = t2 / g.nrb_ce;
+        sweepd_task<K>(a, g.ce[k], t2 - k * g.nrb_ce, g.nrb_ce, g.wlast, lane);
+    }
 }
 
 }  // namespace smi
+
+// One translation unit per K (stencild_k<K>.hip): the eight instantiations
+// compile in parallel.
+#define SMI_SWEEPD_INSTANCE(K)                                                                           \
+    namespace smi {                                                                                      \
+    int sweepd_launch_k##K(const SweepKArgs &a, const SweepDGeom &g, int blocks, hipStream_t s,          \
+                           hipEvent_t start, hipEvent_t stop) {                                          \
+        if (start || stop)                                                                               \
+            hipExtLaunchKernelGGL((sweepd_kernel<K>), dim3(blocks), dim3(256), 0, s, start, stop, 0, a, g); \
+        else                                                                                             \
+            hipLaunchKernelGGL((sweepd_kernel<K>), dim3(blocks), dim3(256), 0, s, a, g);                  \
+        SMI_HIP_CHECK(hipGetLastError());                                                                \
+        return SMI_SUCCESS;                                                                              \
+    }                                                                                                    \
+    int sweepd_resident_k##K() {                                                                         \
+        static int cached[64] = {};                                                                      \
+        int dev = 0;                                                                                     \
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;                          \
+        if (cached[dev]) return cached[dev];                                                             \
+        int per_cu = 0, cus = 0;                                                                         \
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweepd_kernel<K>, 256, 0) != hipSuccess) \
+            return 0;                                                                                    \
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0; \
+        cached[dev] = per_cu * cus * 4;                                                                  \
+        return cached[dev];                                                                              \
+    }                                                                                                    \
+    }

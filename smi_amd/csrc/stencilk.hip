@@ -86,6 +86,27 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
         if (stop) SMI_HIP_CHECK(hipEventRecord(stop, s));
         return SMI_SUCCESS;
     }
+    if (K > SWEEPK_MAX) {
+        // deeper passes: the rotating-ring sweep (stencild.h), single tiles
+        SMI_ARG_CHECK(ht_req <= 0 && reserve <= 0, "sweepk: K > 12 has no row-block / reserve tuning");
+        hipEvent_t start = nullptr, kstop = stop, after = nullptr;
+        int tok = -1;
+        bool marker = false;
+        if (prof && prof_enabled()) {
+            const double units = (double)(a.row_hi - a.row_lo) * (a.col_hi - a.col_lo) * K;
+            if (stop) {
+                SMI_TRY(prof_launch(SMI_PROF_STENCIL_SWEEPK, &tok, K, units, &start, &kstop));
+                after = stop;
+            } else {
+                SMI_TRY(prof_begin(SMI_PROF_STENCIL_SWEEPK, s, &tok, K, units, true));
+                marker = true;
+            }
+        }
+        SMI_TRY(launch_sweepd(K, a, s, start, kstop));
+        if (after) SMI_HIP_CHECK(hipEventRecord(after, s));
+        if (marker) SMI_TRY(prof_end(tok, s));
+        return SMI_SUCCESS;
+    }
     SMI_TRY(check_sweepk(K, a));
     int nstrips = 0, nrb = 0;
     sweepk_geometry(K, a, ht_req, reserve, &nstrips, &nrb);

@@ -131,7 +131,7 @@ def get_bands() -> dict:
 
 
 def set_fusion(steps_per_pass: int = 0, rows_per_wave: int = 0, rows_in_flight: int = 0) -> None:
-    """Up to steps_per_pass (1..12) Jacobi steps fused per pass over HBM
+    """Up to steps_per_pass (1..20) Jacobi steps fused per pass over HBM
     (same bits for every setting); the remainder of a run is one shallower
     pass (smi_stencil_plan)."""
     _lib.call("smi_stencil_set_fusion", steps_per_pass, rows_per_wave, rows_in_flight)
@@ -141,3 +141,16 @@ def get_fusion() -> dict:
     v = [ctypes.c_int() for _ in range(3)]
     _lib.call("smi_stencil_get_fusion", *[ctypes.byref(x) for x in v])
     return dict(steps_per_pass=v[0].value, rows_per_wave=v[1].value, rows_in_flight=v[2].value)
+
+
+def set_deep(ce16: int = -1, rev16: int = -1, waves: int = -1) -> None:
+    """Rotating-ring sweep (K = 13..20) geometry, scheduling only: extra work
+    of edge-column strips / upward bottom blocks in 16ths, waves per launch
+    (0 = one round of resident waves).  -1 keeps a setting."""
+    _lib.call("smi_stencil_set_deep", ce16, rev16, waves)
+
+
+def get_deep() -> dict:
+    v = [ctypes.c_int() for _ in range(3)]
+    _lib.call("smi_stencil_get_deep", *[ctypes.byref(x) for x in v])
+    return dict(ce16=v[0].value, rev16=v[1].value, waves=v[2].value)

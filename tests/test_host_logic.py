@@ -76,24 +76,31 @@ def test_bench_halo_report_counts_neighbours():
 
 # ------------------------------------------------------------ run planner --
 def test_plan_splits_steps_into_balanced_deep_passes():
-    """smi_stencil_plan (host only): a remainder r = T % 12 >= 3 is spread
-    over ceil(T / 12) passes balanced to within one step; r = 1 or 2 stays
-    T // 12 passes of 12 and a pair or a single step."""
+    """smi_stencil_plan (host only), default K = 20 on an 8192^2 single tile:
+    a remainder r = T % 20 >= 3 is spread over ceil(T / 20) passes balanced
+    to within one step; r = 1 or 2 stays T // 20 passes of 20 and a pair or
+    a single step.  Multi-rank tiles clip K to 12 (the band kernel's depth),
+    single tiles shorter than 4K rows too."""
     from smi_amd import stencil
-    for T in range(0, 60):
+    assert stencil.get_fusion()["steps_per_pass"] == 20
+    for T in range(0, 90):
         ph = stencil.plan(8192, 8192, 1, 1, 0, T)["phases"]
         assert sum(k * n for k, n in ph) == T
-        q, r = divmod(T, 12)
+        q, r = divmod(T, 20)
         if r >= 3:
             base, extra = divmod(T, q + 1)
             want = ([(base + 1, extra)] if extra else []) + [(base, q + 1 - extra)]
         else:
-            want = ([(12, q)] if q else []) + ([(r, 1)] if r else [])
+            want = ([(20, q)] if q else []) + ([(r, 1)] if r else [])
         assert ph == want, (T, ph)
-        assert max(k for k, _ in ph or [(0, 0)]) - min(k for k, _ in ph or [(0, 0)]) <= (1 if r >= 3 else 12)
+        assert max(k for k, _ in ph or [(0, 0)]) - min(k for k, _ in ph or [(0, 0)]) <= (1 if r >= 3 else 20)
         assert stencil.plan(8192, 8192, 1, 1, 0, T)["result_index"] == sum(n for _, n in ph) % 2
-    assert stencil.plan(8192, 8192, 1, 1, 0, 20)["phases"] == [(10, 2)]  # the driver's --steps 20
-    assert stencil.plan(8192, 8192, 1, 1, 0, 2400)["phases"] == [(12, 200)]  # bench defaults
+    assert stencil.plan(8192, 8192, 1, 1, 0, 20)["phases"] == [(20, 1)]  # the driver's --steps 20: one pass
+    assert stencil.plan(8192, 8192, 1, 1, 0, 2400)["phases"] == [(20, 120)]  # bench defaults
+    assert stencil.plan(8192, 8192, 2, 4, 3, 20)["phases"] == [(10, 2)]  # multi-rank: K <= 12
+    assert stencil.plan(8192, 8192, 2, 4, 3, 2400)["phases"] == [(12, 200)]
+    assert stencil.plan(79, 512, 1, 1, 0, 20)["phases"] == [(10, 2)]    # shorter than 4 x 20 rows
+    assert stencil.plan(80, 512, 1, 1, 0, 20)["phases"] == [(20, 1)]
 
 
 def test_plan_neighbours_follow_reference_rank_map():

@@ -283,12 +283,13 @@ def test_deep_full_size_8192(gpu, oracle_mod):
     assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 8)))
 
 
-def test_bench_config_full_size_k12(gpu, oracle_mod):
+def test_bench_config_full_size_default_plan(gpu, oracle_mod):
     """BASELINE config 2 exactly as bench.py runs it: 8192^2 fp32, the default
-    K = 12 and automatic row blocks, T = 12 (one pass), 20 (10 + 10: the
-    driver's --steps 20) and 25 (12 + 12 + 1), bit-exact vs the oracle."""
+    K = 20 and automatic geometry, T = 12 (one K = 12 pass), 20 (one pass of
+    the rotating-ring sweep: the driver's --steps 20) and 25 (13 + 12),
+    bit-exact vs the oracle."""
     from smi_amd import LocalGroup, stencil
-    assert stencil.get_fusion()["steps_per_pass"] == 12
+    assert stencil.get_fusion()["steps_per_pass"] == 20
     g = oracle_mod.init_uniform(8192, 8192, seed=1000)
     comm = LocalGroup(1).comm(0)
     want = g
@@ -387,6 +388,71 @@ def test_deep_decomposed_small_tiles(gpu, oracle_mod, k):
     assert np.array_equal(bits(_run_fused(g, 32, 2, 2, k=k)), bits(oracle_mod.stencil_decomposed(g, 32, 2, 2)))
 
 
+# ------------------------- K = 13..20 steps per pass (rotating-ring sweep) --
+# stencild.h: single tiles only (multi-rank runs clip K to 12); tiles shorter
+# than 4K rows clip K to 12 too.
+RING_SHAPES = [(52, 8), (80, 260), (129, 500), (300, 1028), (1000, 516), (257, 2060), (96, 4)]
+
+
+@pytest.mark.parametrize("k", list(range(13, 21)))
+@pytest.mark.parametrize("shape", RING_SHAPES)
+def test_ring_single_tile(gpu, oracle_mod, k, shape):
+    """Every deep K on tiles with one strip (narrower than a window), edge
+    strips on both sides, several interior strips, tall and short row blocks;
+    T = k (one pass), k + 3 and 2k + 1 (balanced passes of mixed depth)."""
+    from smi_amd import stencil
+    X, Y = shape
+    g = oracle_mod.init_uniform(X, Y, seed=X + 7 * Y + k)
+    for T in (k, k + 3, 2 * k + 1):
+        got = _run_fused(g, T, k=k)
+        assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, shape, T)
+    old = stencil.get_fusion()
+    stencil.set_fusion(k)
+    try:
+        ph = stencil.plan(X, Y, 1, 1, 0, k)["phases"]
+    finally:
+        stencil.set_fusion(old["steps_per_pass"])
+    if X >= 4 * k and Y >= 8:
+        assert ph == [(k, 1)], ph   # one deep pass
+    elif Y < 8:
+        assert ph == [(1, k)], ph   # below 4 x 8: single steps
+    else:
+        assert max(kk for kk, _ in ph) <= 12 and sum(kk * n for kk, n in ph) == k, ph
+
+
+@pytest.mark.parametrize("k", [14, 20])
+@pytest.mark.parametrize("geom", [(0, 0, 0), (8, 8, 0), (16, 0, 512), (0, 12, 3000), (3, 4, 64)])
+def test_ring_geometry_is_bit_neutral(gpu, oracle_mod, k, geom):
+    """The edge-strip / bottom-block weights and the wave count of the
+    rotating-ring sweep change scheduling only."""
+    from smi_amd import stencil
+    old = stencil.get_deep()
+    stencil.set_deep(*geom)
+    try:
+        g = oracle_mod.init_uniform(611, 1236, seed=k + geom[0])
+        got = _run_fused(g, 2 * k + 1, k=k)
+        assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 2 * k + 1))), (k, geom)
+    finally:
+        stencil.set_deep(old["ce16"], old["rev16"], old["waves"])
+
+
+def test_ring_config1_edges_and_decomposed(gpu, oracle_mod):
+    """The reference grid (0 interior, 1 on the edges) through K = 16 / 20,
+    and K = 20 asked of a 2x2 run (clipped to the band kernel's 12)."""
+    g = oracle_mod.init_edges(256, 256)
+    for k in (16, 20):
+        assert np.array_equal(bits(_run_fused(g, 32, k=k)), bits(oracle_mod.stencil(g, 32)))
+        assert np.array_equal(bits(_run_fused(g, 32, 2, 2, k=k)), bits(oracle_mod.stencil_decomposed(g, 32, 2, 2)))
+
+
+def test_ring_full_size_8192_driver_config(gpu, oracle_mod):
+    """BASELINE config 2 at the driver's --steps 20 with K = 20: one pass of
+    the rotating-ring sweep over 8192^2, bit-exact vs the oracle."""
+    g = oracle_mod.init_uniform(8192, 8192, seed=1000)
+    got = _run_fused(g, 20, k=20)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, 20)))
+
+
 # ------------------------------------------ special values through every path --
 def _special_grid(X, Y, seed):
     """Uniform grid salted with the values IEEE fp32 treats specially: signed
@@ -415,7 +481,7 @@ def _same(a, b):
     return np.array_equal(na, nb) and np.array_equal(bits(np.where(na, 0, a)), bits(np.where(nb, 0, b)))
 
 
-@pytest.mark.parametrize("k", [1, 2, 4, 12])
+@pytest.mark.parametrize("k", [1, 2, 4, 12, 16, 20])
 @pytest.mark.parametrize("pxpy", [(1, 1), (2, 2)])
 def test_special_values_bit_exact(gpu, oracle_mod, k, pxpy):
     PX, PY = pxpy
@@ -464,20 +530,20 @@ def test_scaled_guard_mixed_blocks(gpu, oracle_mod, pxpy):
         assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (pxpy, T)
 
 
-@pytest.mark.parametrize("k", [3, 7, 12])
+@pytest.mark.parametrize("k", [3, 7, 12, 13, 16, 20])
 def test_scaled_guard_every_k(gpu, oracle_mod, k):
     g = _guard_grid(700, 1028, seed=k)
     assert np.array_equal(bits(_run_fused(g, 2 * k + 1, k=k)), bits(oracle_mod.stencil(g, 2 * k + 1)))
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(10))
 def test_scaled_guard_fuzz(gpu, oracle_mod, seed):
     """Random tiles whose magnitudes span 2^-135 .. 2^110 with mixed signs and
     zeros, in patches, so that within one pass some waves stay in the scaled
     range and others re-walk their blocks exactly; every K, bit-exact."""
     rng = np.random.default_rng(100 + seed)
     X, Y = int(rng.integers(60, 400)), 4 * int(rng.integers(20, 200))
-    k = int(rng.integers(3, 13))
+    k = int(rng.integers(3, 21))
     g = rng.random((X, Y), dtype=np.float32)
     for _ in range(int(rng.integers(1, 6))):  # patches of scaled magnitudes
         r0, c0 = int(rng.integers(0, X)), int(rng.integers(0, Y))
@@ -500,7 +566,12 @@ def test_profiling_entries_distinct(gpu, oracle_mod):
     t = torch.from_numpy(oracle_mod.init_uniform(256, 512, seed=3)).cuda()
     profiling.reset()
     profiling.enable(True)
-    stencil.run(comm, t, 3 * 12 + 5, 1, 1)
+    old = stencil.get_fusion()
+    stencil.set_fusion(12)
+    try:
+        stencil.run(comm, t, 3 * 12 + 5, 1, 1)
+    finally:
+        stencil.set_fusion(old["steps_per_pass"])
     torch.cuda.synchronize()
     profiling.enable(False)
     n = ctypes.c_int()

@@ -85,15 +85,27 @@ int main(int argc, char **argv) {
     hipFuncAttributes fa;
     CK(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(smi::sweepd_kernel<K>)));
     const int waves = per_cu * cus * 4;
-    const int out_rows = n;
-    const int nstrips = (n + sw - 1) / sw;
-    int ht = ht_arg;
-    if (ht <= 0) {
-        const int per_strip = std::max(1, waves / nstrips);
-        ht = std::max(K, (out_rows + per_strip - 1) / per_strip);
+    // the library's geometry (stencild.hip sweepd_geometry), defaults ce16=4, rev16=2
+    const int ce16 = getenv("CE16") ? atoi(getenv("CE16")) + 16 : 20;
+    const int rev16 = getenv("REV16") ? atoi(getenv("REV16")) : 2;
+    smi::SweepDGeom g{};
+    const int KC = S::KC;
+    g.nstrips = (n + sw - 1) / sw;
+    g.ce[0] = g.ce[1] = g.ce[2] = g.ce[3] = -1;
+    int nce = 0;
+    g.int0 = -1;
+    for (int st = 0; st < g.nstrips; ++st) {
+        const int cs = st * sw;
+        if (cs - KC <= 0 || cs - KC + 256 >= n) g.ce[nce++] = st;
+        else { if (g.int0 < 0) g.int0 = st; ++g.n_int; }
     }
-    const int nrb = (out_rows + ht - 1) / ht;
-    const int blocks = (int)(((long)nstrips * nrb + 3) / 4);
+    g.wlast = std::max(4, std::min(16, 256 / (16 + rev16)));
+    int nrb = ht_arg > 0 ? (n + ht_arg - 1) / ht_arg : (int)((long)waves * 16 / ((long)g.n_int * 16 + (long)nce * ce16));
+    g.nrb = nrb;
+    g.nrb_ce = std::max(nrb, nrb * ce16 / 16);
+    g.tasks = g.n_int * g.nrb + nce * g.nrb_ce;
+    const int nstrips = g.nstrips, ht = n / nrb;
+    const int blocks = (g.tasks + 3) / 4;
     bool flip = false;
     auto launch = [&]() {
         smi::SweepKArgs la = args;
@@ -102,7 +114,7 @@ int main(int argc, char **argv) {
             la.out = const_cast<float *>(args.in);
         }
         flip = !flip;
-        hipLaunchKernelGGL((smi::sweepd_kernel<K>), dim3(blocks), dim3(256), 0, 0, la, nstrips, nrb);
+        hipLaunchKernelGGL((smi::sweepd_kernel<K>), dim3(blocks), dim3(256), 0, 0, la, g);
     };
     launch();
     CK(hipDeviceSynchronize());
@@ -118,7 +130,7 @@ int main(int argc, char **argv) {
                 if (r > K && r < n - 1 - K && c > K && c < n - 1 - K) {
                     if (bad_int++ < 8)
                         fprintf(stderr, "interior mismatch (%d,%d) row-in-block %d col-in-strip %d: %a vs %a\n", r, c,
-                                r - (int)((long)(r * (long)nrb) / n * n / nrb), c % sw, got[i], want[i]);
+                                r % ht, c % sw, got[i], want[i]);
                 }
             }
         }
@@ -137,11 +149,11 @@ int main(int argc, char **argv) {
     for (float m : ms) total += m;
     std::sort(ms.begin(), ms.end());
     const double mean = total / launches, med = ms[launches / 2];
-    const double cellsteps = (double)out_rows * n * K;
+    const double cellsteps = (double)n * n * K;
     printf("{\"variant\": \"%s\", \"K\": %d, \"LL\": %d, \"D\": %d, \"B\": %d, \"vgprs\": %d, \"n\": %d, \"ht\": %d, "
            "\"nrb\": %d, \"nstrips\": %d, \"waves\": %d, \"resident\": %d, \"mismatches\": %ld, \"mismatches_interior\": %ld, "
            "\"ms_mean\": %.5f, \"ms_med\": %.5f, \"ms_min\": %.5f, \"GCells\": %.1f, \"compulsory_frac\": %.4f}\n",
-           VARIANT_NAME, K, S::LL, S::D, S::B, fa.numRegs, n, ht, nrb, nstrips, nstrips * nrb, waves, bad, bad_int,
+           VARIANT_NAME, K, S::LL, S::D, S::B, fa.numRegs, n, ht, nrb, nstrips, g.tasks, waves, bad, bad_int,
            mean, med, ms[0], cellsteps / med / 1e6, 8.0 * n * n / (med * 1e-3) / 8e12);
     return bad ? 1 : 0;
 }
