@@ -69,8 +69,9 @@ int smi_stencil_get_tuning(int *rows_per_wave, int *rows_in_flight,
 
 /* Temporal blocking: steps_per_pass = K in 1..20 fuses up to K Jacobi steps
  * into one pass over HBM (same per-cell arithmetic, bit-identical result).
- * K = 13..20 runs the rotating-ring sweep, on single tiles of at least 4K
- * rows (shorter tiles and multi-rank runs clip K to 12).
+ * K = 13..20 runs the rotating-ring sweep, which needs a sweep rectangle
+ * of at least 4K rows (the tile, or a multi-rank interior: the tile minus K
+ * rows per side with a neighbour); K is clipped to 12 otherwise.
  * Multi-rank runs then exchange depth-K halos -- K rows / KC = 4 ceil(K/4)
  * columns per side neighbour and a K x KC corner block per diagonal
  * neighbour -- once per K steps; a band kernel computes the halo-facing bands

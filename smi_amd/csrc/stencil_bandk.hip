@@ -1,5 +1,6 @@
 // stencil_bandk.hip -- host side of the halo-facing bands of a K-step pass
-// (kernel: stencil_bandk.h, one instantiation per K in stencilk_k<K>.hip)
+// (kernel: stencil_bandk.h, one instantiation per K in stencilk_k<K>.hip,
+// K = 13..20 in stencild_k<K>.hip)
 // and the initial depth-K pack.
 #include <cstdlib>
 
@@ -19,12 +20,20 @@ SMI_BANDK_DECL(9)
 SMI_BANDK_DECL(10)
 SMI_BANDK_DECL(11)
 SMI_BANDK_DECL(12)
+SMI_BANDK_DECL(13)
+SMI_BANDK_DECL(14)
+SMI_BANDK_DECL(15)
+SMI_BANDK_DECL(16)
+SMI_BANDK_DECL(17)
+SMI_BANDK_DECL(18)
+SMI_BANDK_DECL(19)
+SMI_BANDK_DECL(20)
 
 int plan_bands(int K, BandKArgs *ap) {
     BandKArgs &a = *ap;
     const int X = a.rows, Y = a.cols;
     a.kc = kc_of(K);
-    SMI_ARG_CHECK(K >= SWEEPK_MIN && K <= SWEEPK_MAX, "bandk: K must be 3..12");
+    SMI_ARG_CHECK(K >= SWEEPK_MIN && K <= SWEEPD_MAX, "bandk: K must be 3..20");
     SMI_ARG_CHECK(X >= 2 * K && Y >= 2 * a.kc && Y % 4 == 0, "bandk: tile smaller than 2K x 2KC");
     // one wave per 64 - 2K cells along a band (stencil_bandk.h)
     a.sw = 64 - 2 * K;
@@ -74,7 +83,15 @@ int launch_bandk(int K, BandKArgs a, int max_waves, hipStream_t s, hipEvent_t st
     case 9: rc = bandk_launch_k9(a, n, s, start, kstop); break;
     case 10: rc = bandk_launch_k10(a, n, s, start, kstop); break;
     case 11: rc = bandk_launch_k11(a, n, s, start, kstop); break;
-    default: rc = bandk_launch_k12(a, n, s, start, kstop); break;
+    case 12: rc = bandk_launch_k12(a, n, s, start, kstop); break;
+    case 13: rc = bandk_launch_k13(a, n, s, start, kstop); break;
+    case 14: rc = bandk_launch_k14(a, n, s, start, kstop); break;
+    case 15: rc = bandk_launch_k15(a, n, s, start, kstop); break;
+    case 16: rc = bandk_launch_k16(a, n, s, start, kstop); break;
+    case 17: rc = bandk_launch_k17(a, n, s, start, kstop); break;
+    case 18: rc = bandk_launch_k18(a, n, s, start, kstop); break;
+    case 19: rc = bandk_launch_k19(a, n, s, start, kstop); break;
+    default: rc = bandk_launch_k20(a, n, s, start, kstop); break;
     }
     SMI_TRY(rc);
     if (after) SMI_HIP_CHECK(hipEventRecord(after, s));

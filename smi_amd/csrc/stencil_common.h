@@ -137,8 +137,9 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht, int reserve, bool prof,
 int sweepk_window_cols(int K);  // output columns per 256-column window
 
 // Deep K-step sweep (stencild.h / stencild.hip, SWEEPD_MIN <= K <= SWEEPD_MAX):
-// same arguments and output as the K-step sweep, for single-tile passes of
-// more than SWEEPK_MAX steps.  The launch geometry: strips of 256 - 2 KC
+// same arguments and output as the K-step sweep (a whole single tile, or a
+// multi-rank interior beside the band kernel), for passes of more than
+// SWEEPK_MAX steps.  The launch geometry: strips of 256 - 2 KC
 // output columns; interior strips cut into nrb row blocks, the strips
 // holding a global-edge column (their waves run the per-lane column copy)
 // into nrb_ce shorter blocks, and in every strip the bottom block of a tile
@@ -167,8 +168,8 @@ __host__ __device__ inline void sweepd_block_rows(const SweepKArgs &a, int rb, i
 }
 bool sweepd_fits(int K, const SweepKArgs &a);
 int sweepd_window_cols(int K);
-int sweepd_geometry(int K, const SweepKArgs &a, SweepDGeom *g);
-int launch_sweepd(int K, const SweepKArgs &a, hipStream_t s, hipEvent_t start, hipEvent_t stop);
+int sweepd_geometry(int K, const SweepKArgs &a, int reserve, SweepDGeom *g);
+int launch_sweepd(int K, const SweepKArgs &a, int reserve, hipStream_t s, hipEvent_t start, hipEvent_t stop);
 
 // Depth-K halos (stencil_bandk.h / stencil_bandk.hip).  KC = 4 ceil(K/4):
 // the column depth, whole float4 groups.  Receive side: top = rows -K..-1 and

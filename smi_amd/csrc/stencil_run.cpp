@@ -217,17 +217,17 @@ static Plan make_plan(int rows, int cols, int timesteps, bool multi) {
     int K = fuse >= SWEEPK_MIN ? fuse : 0;
     if (K && multi) {
         // a multi-rank tile holds the K-row bands and the float4-aligned
-        // K-column bands (4 * ceil(K / 4) wide) of both sides; the band
-        // kernel and the depth-K halos go to SWEEPK_MAX
-        K = std::min({K, rows / 2, SWEEPK_MAX});
+        // K-column bands (4 * ceil(K / 4) wide) of both sides
+        K = std::min(K, rows / 2);
         while (K > 0 && 8 * ((K + 3) / 4) > cols) --K;
     }
-    if (K > SWEEPK_MAX && !multi) {
-        // deep passes (stencild.h) need tall enough tiles: four blocks of K rows
+    if (K > SWEEPK_MAX) {
+        // deep passes (stencild.h) need a tall enough sweep rectangle (a
+        // multi-rank interior loses K rows per side with a neighbour)
         SweepKArgs probe{};
         probe.rows = rows;
         probe.cols = cols;
-        probe.row_hi = rows;
+        probe.row_hi = multi ? rows - 2 * K : rows;
         probe.col_hi = cols;
         if (!sweepd_fits(K, probe)) K = SWEEPK_MAX;
     }

@@ -49,7 +49,7 @@ struct DeepGeom {
 #ifdef SMI_DEEP_D
     static constexpr int D = SMI_DEEP_D;
 #else
-    static constexpr int D = 4;
+    static constexpr int D = 3;  // odd: the cycle 2K + D + 1 splits into groups of two rows
 #endif
 };
 
@@ -66,8 +66,9 @@ struct SweepD {
 #ifdef SMI_DEEP_G
     static constexpr int G = SMI_DEEP_G;
 #else
-    static constexpr int G = 1;
+    static constexpr int G = 2;  // rows per end-of-walk check (K = 20: 0.153 vs 0.162 ms for G = 1)
 #endif
+    static_assert(N % G == 0, "the loop body must hold whole groups");
     static_assert(KC >= K, "apron narrower than the cone");
     static constexpr int kExpLo = 2 * K - 124, kExpHi = 126 - 2 * K;
     static constexpr float kUnscale = 1.0f / (float)(1ull << (2 * K));  // 4^-K, exact
@@ -96,6 +97,10 @@ struct SweepD {
     // backend emits a one-dword buffer_load_dword for it.)
     template <bool REV>
     __device__ __forceinline__ float4 ld(int t) const {
+#ifdef SMI_DEEP_NOMEM  // experiment: levels only, no loads (timing)
+        const float f = (float)(t & 7) * 0.125f + (float)voff_ld * 1e-6f;
+        return make_float4(f, f + 0.25f, f + 0.5f, f + 0.75f);
+#endif
         const int r = __builtin_amdgcn_readfirstlane(min(max(REV ? r_begin - t : r_begin + t, 0), rows - 1));
         const char *rowp = reinterpret_cast<const char *>(in + (size_t)r * cols);
         return *reinterpret_cast<const float4 *>(rowp + (unsigned)voff_ld);

@@ -41,7 +41,7 @@ bool sweepd_fits(int K, const SweepKArgs &a) {
 // waves (or g_tune.deep_waves), the edge-column strips and the bottom
 // blocks shortened by their measured extra cost (g_tune.deep_ce16 /
 // deep_rev16, in 16ths of a block's work).
-int sweepd_geometry(int K, const SweepKArgs &a, SweepDGeom *g) {
+int sweepd_geometry(int K, const SweepKArgs &a, int reserve, SweepDGeom *g) {
     const int KC = 4 * ((K + 3) / 4), SW = sweepd_window_cols(K);
     const int cs0 = a.col_lo & ~31;
     SweepDGeom r{};
@@ -69,6 +69,7 @@ int sweepd_geometry(int K, const SweepKArgs &a, SweepDGeom *g) {
     r.wlast = std::max(4, std::min(16, 256 / (16 + std::max(0, g_tune.deep_rev16))));
     int waves = g_tune.deep_waves > 0 ? g_tune.deep_waves : resident_waves(K);
     SMI_ARG_CHECK(waves > 0, "sweepd: occupancy query failed");
+    if (reserve > 0) waves = std::max(64, waves - reserve);
     int nrb = std::max(1, (int)((long)waves * 16 / ((long)r.n_int * 16 + (long)nce * ce16)));
     const bool both = a.gT && a.gB;
     for (;; --nrb) {
@@ -88,11 +89,13 @@ int sweepd_geometry(int K, const SweepKArgs &a, SweepDGeom *g) {
     return SMI_SUCCESS;
 }
 
-int launch_sweepd(int K, const SweepKArgs &a, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+int launch_sweepd(int K, const SweepKArgs &a, int reserve, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
     SMI_ARG_CHECK(sweepd_fits(K, a), "sweepd: K out of range or tile too short");
     SMI_ARG_CHECK(a.cols % 4 == 0 && a.col_lo % 4 == 0 && a.col_hi % 4 == 0, "sweepd: columns not float4 aligned");
+    SMI_ARG_CHECK(a.row_lo >= 0 && a.row_hi <= a.rows && a.col_lo >= 0 && a.col_hi <= a.cols,
+                  "sweepd: output rectangle outside the tile");
     SweepDGeom g;
-    SMI_TRY(sweepd_geometry(K, a, &g));
+    SMI_TRY(sweepd_geometry(K, a, reserve, &g));
     const int blocks = (g.tasks + 3) / 4;
     switch (K) {
     case 13: return sweepd_launch_k13(a, g, blocks, s, start, stop);

@@ -87,8 +87,10 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
         return SMI_SUCCESS;
     }
     if (K > SWEEPK_MAX) {
-        // deeper passes: the rotating-ring sweep (stencild.h), single tiles
-        SMI_ARG_CHECK(ht_req <= 0 && reserve <= 0, "sweepk: K > 12 has no row-block / reserve tuning");
+        // deeper passes: the rotating-ring sweep (stencild.h); its geometry
+        // has no row-block override, and wave slots reserved for the band
+        // kernel (smi_stencil_set_bands) come off its one round of waves
+        SMI_ARG_CHECK(ht_req <= 0, "sweepk: K > 12 has no row-block override");
         hipEvent_t start = nullptr, kstop = stop, after = nullptr;
         int tok = -1;
         bool marker = false;
@@ -102,7 +104,7 @@ int launch_sweepk_ex(int K, const SweepKArgs &a, int ht_req, int reserve, bool p
                 marker = true;
             }
         }
-        SMI_TRY(launch_sweepd(K, a, s, start, kstop));
+        SMI_TRY(launch_sweepd(K, a, reserve, s, start, kstop));
         if (after) SMI_HIP_CHECK(hipEventRecord(after, s));
         if (marker) SMI_TRY(prof_end(tok, s));
         return SMI_SUCCESS;

@@ -79,8 +79,9 @@ def test_plan_splits_steps_into_balanced_deep_passes():
     """smi_stencil_plan (host only), default K = 20 on an 8192^2 single tile:
     a remainder r = T % 20 >= 3 is spread over ceil(T / 20) passes balanced
     to within one step; r = 1 or 2 stays T // 20 passes of 20 and a pair or
-    a single step.  Multi-rank tiles clip K to 12 (the band kernel's depth),
-    single tiles shorter than 4K rows too."""
+    a single step.  K > 12 needs a sweep rectangle of at least 4K rows (a
+    multi-rank interior loses K rows per side with a neighbour), else K is
+    clipped to 12."""
     from smi_amd import stencil
     assert stencil.get_fusion()["steps_per_pass"] == 20
     for T in range(0, 90):
@@ -97,10 +98,12 @@ def test_plan_splits_steps_into_balanced_deep_passes():
         assert stencil.plan(8192, 8192, 1, 1, 0, T)["result_index"] == sum(n for _, n in ph) % 2
     assert stencil.plan(8192, 8192, 1, 1, 0, 20)["phases"] == [(20, 1)]  # the driver's --steps 20: one pass
     assert stencil.plan(8192, 8192, 1, 1, 0, 2400)["phases"] == [(20, 120)]  # bench defaults
-    assert stencil.plan(8192, 8192, 2, 4, 3, 20)["phases"] == [(10, 2)]  # multi-rank: K <= 12
-    assert stencil.plan(8192, 8192, 2, 4, 3, 2400)["phases"] == [(12, 200)]
+    assert stencil.plan(8192, 8192, 2, 4, 3, 20)["phases"] == [(20, 1)]  # multi-rank interior: deep too
+    assert stencil.plan(8192, 8192, 2, 4, 3, 2400)["phases"] == [(20, 120)]
     assert stencil.plan(79, 512, 1, 1, 0, 20)["phases"] == [(10, 2)]    # shorter than 4 x 20 rows
     assert stencil.plan(80, 512, 1, 1, 0, 20)["phases"] == [(20, 1)]
+    assert stencil.plan(119, 512, 2, 2, 0, 20)["phases"] == [(10, 2)]   # interior (rows - 2K) under 4K
+    assert stencil.plan(120, 512, 2, 2, 0, 20)["phases"] == [(20, 1)]
 
 
 def test_plan_neighbours_follow_reference_rank_map():

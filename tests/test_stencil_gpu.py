@@ -438,11 +438,50 @@ def test_ring_geometry_is_bit_neutral(gpu, oracle_mod, k, geom):
 
 def test_ring_config1_edges_and_decomposed(gpu, oracle_mod):
     """The reference grid (0 interior, 1 on the edges) through K = 16 / 20,
-    and K = 20 asked of a 2x2 run (clipped to the band kernel's 12)."""
+    single tile and as the 2x2 emulator program (128^2 tiles: interiors of
+    88 rows, deep enough for K = 20)."""
     g = oracle_mod.init_edges(256, 256)
     for k in (16, 20):
         assert np.array_equal(bits(_run_fused(g, 32, k=k)), bits(oracle_mod.stencil(g, 32)))
         assert np.array_equal(bits(_run_fused(g, 32, 2, 2, k=k)), bits(oracle_mod.stencil_decomposed(g, 32, 2, 2)))
+
+
+@pytest.mark.parametrize("overlap", [0, 1])
+@pytest.mark.parametrize("k", [13, 16, 20])
+@pytest.mark.parametrize("pxpy", [(2, 1), (1, 2), (2, 2), (3, 3), (2, 4)])
+def test_ring_decomposed(gpu, oracle_mod, k, pxpy, overlap):
+    """Multi-rank K-step passes with the rotating-ring interior, the depth-K
+    band kernel, depth-K halos and K x KC corner blocks (tiles 136 x 264: the
+    interior keeps >= 4K rows), then the remainder phases (T = 2K + 3)."""
+    from smi_amd import stencil
+    PX, PY = pxpy
+    g = oracle_mod.init_uniform(136 * PX, 264 * PY, seed=PX * 13 + PY + k)
+    old = stencil.get_fusion()
+    stencil.set_fusion(k)
+    try:
+        assert stencil.plan(136, 264, PX, PY, 0, k)["phases"] == [(k, 1)]
+    finally:
+        stencil.set_fusion(old["steps_per_pass"])
+    for T in (k, 2 * k + 3):
+        got = _run_fused(g, T, PX, PY, overlap, k=k)
+        assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, pxpy, T)
+
+
+@pytest.mark.parametrize("k", [16, 20])
+@pytest.mark.parametrize("bands", [(0, 1), (64, 1), (500, 1)])
+def test_ring_band_reserve_is_bit_neutral(gpu, oracle_mod, k, bands):
+    """Wave slots reserved for the band kernel come off the rotating-ring
+    interior's round of waves: scheduling only."""
+    from smi_amd import stencil
+    old = stencil.get_bands()
+    stencil.set_bands(*bands)
+    try:
+        g = oracle_mod.init_uniform(3 * 140, 3 * 264, seed=k + bands[0] % 97)
+        for overlap in (1, 0):
+            got = _run_fused(g, k + 1, 3, 3, overlap, k=k)
+            assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, k + 1))), (k, bands, overlap)
+    finally:
+        stencil.set_bands(old["reserve_waves"], old["interior_rounds"])
 
 
 def test_ring_full_size_8192_driver_config(gpu, oracle_mod):
