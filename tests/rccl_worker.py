@@ -114,7 +114,7 @@ def stencil_cases(comm, rank, world, s):
     for T in (13, 27):
         want = oracle.stencil(g, T) if rank == 0 else None
         for overlap in (1, 0):
-            for fuse in (1, 2, 12):
+            for fuse in (1, 2, 12, 20):
                 stencil.set_tuning(overlap=overlap)
                 stencil.set_fusion(steps_per_pass=fuse)
                 t = torch.from_numpy(tiles[rank]).cuda()
@@ -127,7 +127,7 @@ def stencil_cases(comm, rank, world, s):
                     report(rank, f"stencil {PX}x{PY} T={T} overlap={overlap} K={fuse}",
                            np.array_equal(got.view(np.uint32), want.view(np.uint32)))
     stencil.set_tuning(overlap=1)
-    stencil.set_fusion(steps_per_pass=12)
+    stencil.set_fusion(steps_per_pass=20)
 
 
 def channel_cases(comm, rank, world, s):

@@ -1,8 +1,10 @@
 """BASELINE configs 3-5 at their full size on one GPU (in-process rank groups).
 
 * Config 3 (examples/CMakeLists.txt:2-7, stencil_smi 16384^2 as 2x2 and 2x4):
-  4 ranks x 8192^2 and 8 ranks x 8192x4096 tiles, T = 2K+3 steps (two K=12
-  passes with halo exchanges, then the remainder), bit-exact vs the oracle.
+  4 ranks x 8192^2 and 8 ranks x 8192x4096 tiles, T = 43 steps under the
+  default K = 20 (three balanced passes of 15 + 14 + 14 steps: the
+  rotating-ring interior, depth-K bands and halo exchanges), bit-exact vs
+  the oracle.
 * Config 4 (microbenchmarks reduce/bcast, 64 MiB and 256 MiB, 8 ranks): the
   rank+1 known answer of test/reduce/reduce.cl:7-61 on every element, and
   random contributions checked against the oracle's canonical rank-order fold
@@ -28,10 +30,13 @@ def bits(a):
 def test_config3_stencil_16384(gpu, oracle_mod, pxpy):
     from smi_amd import LocalGroup, stencil
     PX, PY = pxpy
-    N, T = 16384, 2 * 12 + 3
+    # the default plan (K = 20): T = 43 as three balanced passes of the
+    # rotating-ring interior with depth-15 / depth-14 halo exchanges
+    assert stencil.get_fusion()["steps_per_pass"] == 20
+    N, T = 16384, 2 * 20 + 3
     g = oracle_mod.init_uniform(N, N, seed=33 + PY)
     tiles = stencil.split_memory(g, PX, PY)
-    stencil.set_fusion(12, -1)
+    assert stencil.plan(N // PX, N // PY, PX, PY, 0, T)["phases"] == [(15, 1), (14, 2)]
 
     def rank_fn(comm):
         s = torch.cuda.Stream()
