@@ -81,8 +81,8 @@ struct Tuning {
     // an upward-walking bottom block's waves, in 16ths of a plain block's
     // (their blocks are shortened by it); waves of the launch (0 = one round
     // of resident waves)
-    int deep_ce16 = 4;
-    int deep_rev16 = 2;
+    int deep_ce16 = 10;  // tools/deep_tune.py: K = 20 at 8192^2, 0.141 ms (4/2: 0.156)
+    int deep_rev16 = 6;
     int deep_waves = 0;
 };
 extern Tuning g_tune;

@@ -413,11 +413,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     int cur = 0;  // index of the buffer holding the current state
     auto bufp = [&](int i) { return i ? buf1 : buf0; };
 
-    hipEvent_t ev_edge, ev_int;
-    SMI_TRY(comm_event(c, 0, &ev_edge));
-    SMI_TRY(comm_event(c, 1, &ev_int));
-
-    if (side_mask == 0) {  // single tile: no halos, no exchange
+    if (side_mask == 0) {  // single tile: no halos, no exchange, no events
         for (int ph = 0; ph < plan.nph; ++ph) {
             const int K = plan.k[ph];
             SweepKArgs ak = interior_args(K);
@@ -439,6 +435,10 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
         }
         return SMI_SUCCESS;
     }
+
+    hipEvent_t ev_edge, ev_int;
+    SMI_TRY(comm_event(c, 0, &ev_edge));
+    SMI_TRY(comm_event(c, 1, &ev_int));
 
     // Halo staging.  Depth 2 (its inner row/column doubles as the depth-1
     // halo): top2 | bot2 | left2 | right2 | corner(4) | send_left2 |

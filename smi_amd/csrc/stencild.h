@@ -46,10 +46,21 @@ struct DeepGeom {
 #else
     static constexpr int LL = (K + 3) / 4;
 #endif
+#ifdef SMI_DEEP_PAIR
+    static constexpr bool PAIR = SMI_DEEP_PAIR;
+#else
+    // rows in interleaved pairs (SweepD::pair): off -- 1.5 % faster in the
+    // interior-only timing variant at K = 20 with D = 7, 2.4 % slower in the
+    // full kernel (236 vs 220 VGPRs; tools/deepbench interleaved A/B)
+    static constexpr bool PAIR = false;
+#endif
 #ifdef SMI_DEEP_D
     static constexpr int D = SMI_DEEP_D;
 #else
-    static constexpr int D = 3;  // odd: the cycle 2K + D + 1 splits into groups of two rows
+    // odd (the cycle 2K + D + 1 splits into pairs of rows); K <= 16 keeps 3
+    // to stay at 3 waves/SIMD, the pairs of the deeper K want more rows in
+    // flight (a pair issues its second row's load late)
+    static constexpr int D = PAIR ? 7 : 3;
 #endif
 };
 
@@ -60,6 +71,7 @@ struct SweepD {
     static constexpr int LL = Geom::LL;
     static constexpr int KC = 4 * LL;
     static constexpr int D = Geom::D;       // rows loaded ahead
+    static constexpr bool PAIR = Geom::PAIR; // rows processed in interleaved pairs
     static constexpr int N = 2 * K + D + 1;  // cycle length (registers, loop body rows)
     static constexpr int PRO = 2 * K + 1;    // prologue rows (the last stores the first output row)
     static constexpr int B = N;
@@ -296,18 +308,18 @@ struct SweepD {
             // the walk's end is checked every G rows: the rows of a group
             // schedule together (a row past the end loads the clamped last row
             // and stores nothing)
-#ifdef SMI_DEEP_PAIR
+            if constexpr (PAIR) {
             static_assert(N % 2 == 0, "pairs of rows need an even cycle (D odd)");
             if (t + r >= n_in) return false;
             pair<REV, CE, SC, (J0 + r) % N, -1>(t + r);
             return body<REV, CE, SC, r + 2, J0>(t);
-#else
+            } else {
             if constexpr (r % G == 0) {
                 if (t + r >= n_in) return false;
             }
             row<REV, CE, SC, (J0 + r) % N, -1>(t + r);
             return body<REV, CE, SC, r + 1, J0>(t);
-#endif
+            }
         }
     }
 
@@ -326,22 +338,22 @@ struct SweepD {
             if (!body<REV, CE, SC, 0, 0>(t)) break;
 #else
         // prologue: input rows 0 .. 2K, compile-time t (rotation j = t)
-#ifdef SMI_DEEP_PAIR
-        row<REV, CE, SC, 0, 0>(0);
-        static_for<K>([&](auto P) {
-            constexpr int t = 2 * P + 1;
-            __builtin_amdgcn_sched_barrier(0);
-            pair<REV, CE, SC, t % N, t>(t);
-        });
-#else
-        static_for<PRO>([&](auto T) {
-            constexpr int t = T;
-            // scheduling regions of G rows, as in the loop (one region of
-            // 2K+1 rows costs minutes of compile time for nothing)
-            if constexpr (t % G == 0 && t > 0) __builtin_amdgcn_sched_barrier(0);
-            row<REV, CE, SC, t % N, t>(t);
-        });
-#endif
+        if constexpr (PAIR) {
+            row<REV, CE, SC, 0, 0>(0);
+            static_for<K>([&](auto P) {
+                constexpr int t = 2 * P + 1;
+                __builtin_amdgcn_sched_barrier(0);
+                pair<REV, CE, SC, t % N, t>(t);
+            });
+        } else {
+            static_for<PRO>([&](auto T) {
+                constexpr int t = T;
+                // scheduling regions of G rows, as in the loop (one region of
+                // 2K+1 rows costs minutes of compile time for nothing)
+                if constexpr (t % G == 0 && t > 0) __builtin_amdgcn_sched_barrier(0);
+                row<REV, CE, SC, t % N, t>(t);
+            });
+        }
         // steady state: N rows per iteration from rotation PRO mod N
         for (int t = PRO;; t += N)
             if (!body<REV, CE, SC, 0, PRO % N>(t)) break;

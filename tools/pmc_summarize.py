@@ -5,7 +5,7 @@
   pmc_summarize.py driver <kernel_stats.csv> <command> <out.json>
   pmc_summarize.py pmc  <fetch_counter_collection.csv> <write_counter_collection.csv> <cells> <out.json> [K]
 
-With K >= 3 only the dispatches of sweepk_kernel<K> count, and the result is
+With K >= 3 only the dispatches of sweepk_kernel<K> (K > 12: sweepd_kernel<K>) count, and the result is
 merged into <out.json>'s "entries" (one per steps-per-launch), which is what
 bench.py looks its roofline traffic up in.
 
@@ -61,13 +61,14 @@ def main():
         return
     cells = int(sys.argv[4])
     steps_per_launch = int(sys.argv[6]) if len(sys.argv) > 6 else 1
-    kern = f"sweepk_kernel<{steps_per_launch}>" if steps_per_launch >= 3 else KERNEL
+    kname = "sweepd_kernel" if steps_per_launch > 12 else "sweepk_kernel"  # K > 12: stencild.h
+    kern = f"{kname}<{steps_per_launch}>" if steps_per_launch >= 3 else KERNEL
     fetch = counter_per_dispatch(sys.argv[2], "FETCH_SIZE", kern)
     write = counter_per_dispatch(sys.argv[3], "WRITE_SIZE", kern)
     f = sorted(fetch)[len(fetch) // 2]
     w = sorted(write)[len(write) // 2]
     d = {
-        "kernel": {1: "sweep_kernel", 2: "sweep2_kernel"}.get(steps_per_launch, f"sweepk_kernel<{steps_per_launch}>"),
+        "kernel": {1: "sweep_kernel", 2: "sweep2_kernel"}.get(steps_per_launch, f"{kname}<{steps_per_launch}>"),
         "cells": cells,
         "dispatches": [len(fetch), len(write)],
         "FETCH_SIZE_KiB_median": f,
