@@ -30,3 +30,8 @@ def test_bench_self_launch_two_ranks(gpu):
     assert d["config"]["decomposition"] == [1, 2] and d["config"]["fake_host"]
     assert d["config"]["launch"].startswith("self")
     assert d["roofline"]["kernels"], d["roofline"]
+    # the timed plan re-run from the seeded inputs and checked per rank on its
+    # light cone against the oracle, verdict agreed by both ranks
+    p = d["parity"]
+    assert p["checked"] and p["bit_exact"] and p["mismatches"] == 0, p
+    assert p["cells"] == 2 * 2048 * 2048 and p["steps"] == 24 and p["same_plan_as_timed"], p
