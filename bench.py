@@ -79,6 +79,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PEAK_TADDS = 78.6         # MI355X_MICROARCH.md: FP32 vector 157.3 TFLOPS spec (FMA = 2) -> adds/s
 BYTES_PER_CELL = 8             # one fp32 read + one fp32 write per cell per step
 TILE = 8192                    # per-GPU tile edge (BASELINE config 2 / weak scaling)
 DECOMP = {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}
@@ -952,13 +953,23 @@ def main() -> None:
     if dom:
         rp = (rocprof_avg(f"{'sweepd' if spl > 12 else 'sweepk'}_kernel<{spl}>")
               if dom["kind"] == profiling.SWEEPK else None)
-        if rp:
+        if rp and world == 1:  # the committed summary is of the N = 1 driver command
             rp["ratio_to_hip_events"] = round(rp["avg_ms"] / sweep_avg_ms, 4) if sweep_avg_ms else None
             out["roofline"]["rocprof"] = rp
     if traffic and sweep_avg_ms:
         hbm = traffic / (sweep_avg_ms * 1e-3) / 1e9
         out["roofline"]["hbm_achieved"] = round(hbm, 1)
         out["roofline"]["hbm_frac"] = round(hbm / HBM_PEAK_GBS, 4)  # per GPU
+    if sweep_avg_ms and spl:
+        # The VALU side of the same launch: algorithmic fp32 adds (3 per
+        # cell-step, ((S+W)+E)+N; the scaled levels drop the reference's x0.25
+        # per step) over the FP32 vector add rate (157.3 TFLOPS spec counts an
+        # FMA as 2: 32 lanes x 1024 SIMDs x 2.4 GHz = 78.6 T adds/s).
+        adds = 3.0 * cells_launch * spl / (sweep_avg_ms * 1e-3) / 1e12
+        out["roofline"]["valu"] = {"achieved": round(adds, 2), "peak": VALU_PEAK_TADDS, "unit": "T fp32 adds/s",
+                                   "frac": round(adds / VALU_PEAK_TADDS, 4),
+                                   "note": "3 adds per cell-step x cells x K per launch / avg launch time; the issued "
+                                           "VALU count (SQ_INSTS_VALU) is in profiles/r04/sq_driver.txt"}
     if world > 1:
         out["halo"] = halo_report(PX, PY, X, Y, max(spl, 1), elapsed / args.steps * 1e3)
     if not args.no_parity:
