@@ -98,6 +98,14 @@ int smi_stencil_get_fusion(int *steps_per_pass, int *rows_per_wave, int *rows_in
 int smi_stencil_set_bands(int reserve_waves, int interior_rounds);
 int smi_stencil_get_bands(int *reserve_waves, int *interior_rounds);
 
+/* Multi-rank K-step passes with K >= 13 (scheduling only, bit-neutral): the
+ * kernel that computes the halo-facing bands.  1 (default) = the lean kernel
+ * (<= 64 VGPRs, one workgroup per CU, its levels staged through LDS) that
+ * runs beside the interior sweep; 0 = one wave per band segment, which only
+ * finds wave slots in the interior's tail.  lean = -1 keeps the setting. */
+int smi_stencil_set_band_kernel(int lean);
+int smi_stencil_get_band_kernel(int *lean);
+
 /* The rotating-ring sweep (K = 13..20) launches one round of waves whose
  * row blocks are shortened where a wave has more work per row: ce16 / rev16
  * = the extra work of a wave holding a global-edge column / of the

@@ -34,7 +34,8 @@ CXXFLAGS = [
 # vectorizer would pack the shuffled (S+W)/(+E) adds too and pay a register
 # move for each pair (the rotating-ring sweep ran 0.217 instead of ~0.15 ms
 # per K = 20 pass without this flag).
-FILE_FLAGS = {"stencilk_k": ["-fno-slp-vectorize"], "stencild_k": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"stencilk_k": ["-fno-slp-vectorize"], "stencild_k": ["-fno-slp-vectorize"],
+              "bandk_k": ["-fno-slp-vectorize"]}
 # Build variants, each in its own directory: the product library (no
 # experiment switch is compiled into it), a bounds-checked diagnostic build,
 # the loopback rehearsal build (tools/rehearsal.py: SMI_LOOPBACK* switches)
@@ -51,8 +52,9 @@ VARIANT_FLAGS = {
 # Sources no variant switch reaches (no SMI_LOOPBACK* / SMI_BOUNDS_CHECK /
 # SMI_EXPERIMENTS in them or in what they include): every variant links the
 # release objects of these instead of compiling them again (the rotating-ring
-# sweep's eight instantiation units take minutes each).
-SHARED_PREFIXES = ("stencild_k",)
+# sweep's eight instantiation units take minutes each; the K-step sweeps'
+# and the band kernels' too).
+SHARED_PREFIXES = ("stencild_k", "stencilk_k", "bandk_k")
 
 
 def file_flags(src: str) -> list[str]:

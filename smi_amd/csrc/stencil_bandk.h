@@ -1,6 +1,6 @@
 // stencil_bandk.h -- the halo-facing bands of a multi-rank K-step pass as
-// short register walks, one cell per lane (instantiated per K beside
-// sweepk_kernel<K> in stencilk_k<K>.hip).
+// short register walks, one cell per lane (instantiated per K in
+// bandk_k<K>.hip; the lean variant bandl_kernel<K> for K = 13..20).
 //
 // In a multi-rank run with K steps per pass, every tile cell within K rows of
 // a side with a neighbour, or within KC = 4 ceil(K/4) columns of one, depends
@@ -253,6 +253,289 @@ __global__ __launch_bounds__(256) void bandk_kernel(BandKArgs a) {
         bandk_wave<K>(a, wv, threadIdx.x & 63);
 }
 
+// ---------------------------------------------------------------------------
+// The lean band kernel (K = 13..20, round 4): the same cells, the same
+// arithmetic and the same stores as BandW, shaped to run BESIDE the deep
+// interior sweep instead of in its tail.  sweepd_kernel<20> holds 2 waves per
+// SIMD at 219 VGPRs (448 of the SIMD's 512), so a wave of <= 64 VGPRs still
+// fits next to them; BandW<20> needs 249 (every input loaded up front, a
+// K-level ring) and only gets slots as interior waves retire, which puts the
+// bands -- and the exchange behind them -- on the pass boundary.  Beside the
+// interior the band kernel's VALU work slows the interior down, so it is
+// also cut: a lane owns TWO cells (columns 2l, 2l+1 of a 128-column window in
+// the row walks, rows 2l, 2l+1 in the column walks), the neighbour across
+// the pair comes from the lane itself, and a wave stores 128 - 2KE cells
+// (KE = K rounded up to even: pair-aligned windows) instead of 64 - 2K:
+// 88 instead of 24 at K = 20, ~2.5x less VALU per band cell.
+//
+// A streaming walk holds two values per level and cell: too many for 64
+// VGPRs.  So each wave walks its segment in KS = ceil(K/5) stages of at most
+// 5 levels: the first from the streamed inputs, its level-L0 values of
+// positions [L0, N-L0) parked in LDS (lane-private columns), each later stage
+// reading the previous one's parked values and overwriting them in place.
+// Level l at walk position p always reads level l-1 at p-1, p, p+1, so a
+// stage is the same recurrence on a shorter input -- bit-identical.
+// Each workgroup reserves more than half a CU's LDS (kBandLeanLds), so at
+// most one workgroup -- one wave per SIMD -- sits on a CU: the interior's two
+// waves per SIMD always fit beside it.  The grid is at most one workgroup per
+// CU, its waves looping over the band segments.
+template <int K>
+struct BandL {
+    using B = BandW<K>;
+    static constexpr int KC = B::KC, NR = B::NR, NC = B::NC, G4 = B::G4;
+    static constexpr int KE = K + (K & 1);   // pair-aligned cone margin
+    static constexpr int SW = 128 - 2 * KE;  // cells stored per wave (segment length)
+    static constexpr int LMAX = 5;
+    static constexpr int KS = (K + LMAX - 1) / LMAX;
+    static constexpr int lv(int s) { return K / KS + (s < K % KS ? 1 : 0); }
+    static constexpr int L0 = lv(0);
+    static constexpr int NPOS = (NR > NC ? NR : NC) - 2 * L0;  // parked positions (x 2 cells) per lane
+    static constexpr int LA = 3;                                // global inputs loaded ahead
+    static constexpr int LAS = 2;                               // parked values read ahead
+
+    // One level step of a lane's two cells (reference order 0.25 *
+    // (((S + W) + E) + N) each).  ROWWALK: cells = columns (a | b), W / E of
+    // a = b of lane-1 / own b, of b = own a / a of lane+1; else cells = rows,
+    // N / S of a = b of lane-1 / own b, of b = own a / a of lane+1.
+    template <bool ROWWALK>
+    __device__ __forceinline__ static float2 cell2(float2 older, float2 c, float2 newer) {
+        if constexpr (ROWWALK)
+            return make_float2(jacobi(newer.x, shr1_any(c.y), c.y, older.x),
+                               jacobi(newer.y, c.x, shl1_any(c.x), older.y));
+        else
+            return make_float2(jacobi(c.y, older.x, newer.x, shr1_any(c.y)),
+                               jacobi(shl1_any(c.x), older.y, newer.y, c.x));
+    }
+
+    // Levels 1..LV over N inputs: ld(t) yields input t (issuing its own
+    // loads ahead), out(q, v) takes the level-LV values of input t = q + 2LV.
+    // cp: per cell, the copy rule (a global edge across the walk).
+    template <bool ROWWALK, bool CP, int N, int LV, typename Ld, typename Out>
+    __device__ __forceinline__ static void walk(bool cpa, bool cpb, Ld &&ld, Out &&out) {
+        float2 W[LV][3];
+        static_for<N>([&](auto T) {
+            constexpr int t = T;
+            W[0][t % 3] = ld(T);
+            float2 v = make_float2(0.0f, 0.0f);
+            static_for<LV>([&](auto L) {
+                constexpr int l = L + 1;
+                if constexpr (t >= 2 * l) {
+                    const float2 c = W[l - 1][(t + 2) % 3];
+                    v = cell2<ROWWALK>(W[l - 1][(t + 1) % 3], c, W[l - 1][t % 3]);
+                    if constexpr (CP) {
+                        v.x = cpa ? c.x : v.x;
+                        v.y = cpb ? c.y : v.y;
+                    }
+                    if constexpr (l < LV) W[l][t % 3] = v;
+                    // (a region per level: the scheduler would otherwise
+                    // start every level's shuffles at once and spill)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            });
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (t >= 2 * LV) out(std::integral_constant<int, t - 2 * LV>{}, v);
+        });
+    }
+
+    // Stages S.. over the N parked positions of the previous stage (in place:
+    // stage output u is written after input u + 2LV was read); the last
+    // stage hands its values to out.
+    template <bool ROWWALK, bool CP, int S, int N, typename Out>
+    __device__ __forceinline__ static void stages(bool cpa, bool cpb, float2 *park, int lane, Out &&out) {
+        constexpr int LV = lv(S);
+        // the previous stage's values go through LDS: without this barrier
+        // the compiler forwards every parked value to its reload and keeps
+        // them all in registers (and spills)
+        asm volatile("" ::: "memory");
+        float2 y[N];
+        static_for<LAS>([&](auto U) { y[U] = park[U * 64 + lane]; });
+        auto ld = [&](auto U) {
+            constexpr int u = U;
+            if constexpr (u + LAS < N) y[u + LAS] = park[(u + LAS) * 64 + lane];
+            return y[u];
+        };
+        if constexpr (S + 1 == KS) {
+            walk<ROWWALK, CP, N, LV>(cpa, cpb, ld, out);
+        } else {
+            walk<ROWWALK, CP, N, LV>(cpa, cpb, ld, [&](auto U, float2 v) { park[U * 64 + lane] = v; });
+            stages<ROWWALK, CP, S + 1, N - 2 * LV>(cpa, cpb, park, lane, out);
+        }
+    }
+
+    // top (BOT = false) or bottom band: lane = columns c, c + 1, rows r0 + t
+    template <bool BOT, bool CP>
+    __device__ __forceinline__ static void rows(const BandKArgs &a, int w, int lane, float2 *park) {
+        const int X = a.rows, Y = a.cols;
+        const int c = w * SW - KE + 2 * lane;  // even: a pair never straddles a region
+        const int r0 = BOT ? X - 2 * K : -K;
+        const int th = BOT ? 2 * K : 0;
+        const int tt = BOT ? 0 : K;
+        const BandSrc src(a, K);
+        // lanes past a global edge read any pair of the tile (their cells
+        // only feed cells the copy rule overrides)
+        const int cl = min(max(c, a.has[2] ? -KC : 0), a.has[3] ? Y + KC - 2 : Y - 2);
+        const float *ph = src.at(r0 + th, cl);
+        const float *pt = src.at(r0 + tt, cl);
+        const int sh = (int)(src.at(r0 + th + 1, cl) - ph);
+        const int st = (int)(src.at(r0 + tt + 1, cl) - pt);
+        auto gload = [&](auto T) -> float2 {
+            constexpr int t = T;
+            constexpr bool halo = BOT ? t >= 2 * K : t < K;
+            return *reinterpret_cast<const float2 *>(halo ? ph + (t - th) * sh : pt + (t - tt) * st);
+        };
+        const bool store = lane >= KE / 2 && lane < 64 - KE / 2 && c < Y;
+        const bool cpa = !a.has[2] && c == 0;
+        const bool cpb = !a.has[3] && c + 1 == Y - 1;
+        float2 x[NR];
+        static_for<LA>([&](auto T) { x[T] = gload(T); });
+        walk<true, CP, NR, L0>(
+            cpa, cpb,
+            [&](auto T) {
+                constexpr int t = T;
+                if constexpr (t + LA < NR) x[t + LA] = gload(std::integral_constant<int, t + LA>{});
+                return x[t];
+            },
+            [&](auto U, float2 v) { park[U * 64 + lane] = v; });
+        const int KCr = a.kc;
+        stages<true, CP, 1, NR - 2 * L0>(cpa, cpb, park, lane, [&](auto Q, float2 v) {
+            constexpr int q = Q;  // output row r0 + K + q
+            if (!store) return;
+            const int r = r0 + K + q;
+            *reinterpret_cast<float2 *>(a.out + (size_t)r * Y + c) = v;
+            if (!a.pack) return;
+            // KCr and Y - KCr are multiples of 4: the pair lies on one side
+            if (c < KCr) {
+                *reinterpret_cast<float2 *>(a.h.send_left + (size_t)r * KCr + c) = v;
+                *reinterpret_cast<float2 *>(a.h.send_corner[BOT ? 2 : 0] + q * KCr + c) = v;
+            }
+            if (c >= Y - KCr) {
+                *reinterpret_cast<float2 *>(a.h.send_right + (size_t)r * KCr + c - (Y - KCr)) = v;
+                *reinterpret_cast<float2 *>(a.h.send_corner[BOT ? 3 : 1] + q * KCr + c - (Y - KCr)) = v;
+            }
+        });
+    }
+
+    // left (RIGHT = false) or right band: lane = rows r, r + 1, columns c0 + t
+    template <bool RIGHT, bool CP>
+    __device__ __forceinline__ static void cols(const BandKArgs &a, int w, int lane, float2 *park) {
+        const int X = a.rows, Y = a.cols;
+        const int r = a.rlo + w * SW - KE + 2 * lane;
+        const int g0 = RIGHT ? Y - 2 * KC : -KC;
+        const BandSrc src(a, K);
+        // per row two contiguous runs: left band: halo columns [-KC, 0) then
+        // tile columns [0, 2KC); right band: tile [Y-2KC, Y) then halo
+        // [Y, Y+KC) (a band exists only beside a neighbour)
+        constexpr int JB = RIGHT ? 2 * KC / 4 : KC / 4;  // first group of the second run
+        const float *pa0 = src.at(r, g0), *pb0 = src.at(r, g0 + 4 * JB);
+        const float *pa1 = src.at(r + 1, g0), *pb1 = src.at(r + 1, g0 + 4 * JB);
+        auto ldg = [&](auto J, const float *pa, const float *pb) {
+            constexpr int j = J;
+            return *reinterpret_cast<const float4 *>(j < JB ? pa + 4 * j : pb + 4 * (j - JB));
+        };
+        constexpr int E0 = KC - K;  // walk input t is element E0 + t of the groups
+        const bool store = lane >= KE / 2 && lane < 64 - KE / 2;
+        const bool st0 = store && r < a.rhi, st1 = store && r + 1 < a.rhi;
+        const bool cpa = (!a.has[0] && r == 0) || (!a.has[1] && r == X - 1);
+        const bool cpb = (!a.has[0] && r + 1 == 0) || (!a.has[1] && r + 1 == X - 1);
+        float4 g0r[G4], g1r[G4];
+        auto fetch = [&](auto J) {
+            g0r[J] = ldg(J, pa0, pb0);
+            g1r[J] = ldg(J, pa1, pb1);
+        };
+        fetch(std::integral_constant<int, E0 / 4>{});
+        if constexpr (E0 / 4 + 1 < G4) fetch(std::integral_constant<int, E0 / 4 + 1>{});
+        auto comp = [](const float4 &q4, int e) { return e == 0 ? q4.x : e == 1 ? q4.y : e == 2 ? q4.z : q4.w; };
+        walk<false, CP, NC, L0>(
+            cpa, cpb,
+            [&](auto T) {
+                constexpr int t = T, e = E0 + t;
+                // entering group e/4: fetch the one after the next
+                if constexpr (e % 4 == 0 || t == 0)
+                    if constexpr (e / 4 + 2 < G4) fetch(std::integral_constant<int, e / 4 + 2>{});
+                return make_float2(comp(g0r[e / 4], e % 4), comp(g1r[e / 4], e % 4));
+            },
+            [&](auto U, float2 v) { park[U * 64 + lane] = v; });
+        const int c0 = RIGHT ? Y - KC : 0;
+        float *send = RIGHT ? a.h.send_right : a.h.send_left;
+        float2 o[4];
+        auto put = [&](int rr, float4 vv, int j) {
+            *reinterpret_cast<float4 *>(a.out + (size_t)rr * Y + c0 + j) = vv;
+            if (!a.pack) return;
+            *reinterpret_cast<float4 *>(send + (size_t)rr * KC + j) = vv;
+            if (rr < K) *reinterpret_cast<float4 *>(a.h.send_corner[RIGHT ? 1 : 0] + rr * KC + j) = vv;
+            if (rr >= X - K) *reinterpret_cast<float4 *>(a.h.send_corner[RIGHT ? 3 : 2] + (rr - (X - K)) * KC + j) = vv;
+        };
+        stages<false, CP, 1, NC - 2 * L0>(cpa, cpb, park, lane, [&](auto Q, float2 v) {
+            constexpr int q = Q;  // output column c0 + q
+            o[q % 4] = v;
+            if constexpr (q % 4 == 3) {
+                constexpr int j = q - 3;
+                if (st0) put(r, make_float4(o[0].x, o[1].x, o[2].x, o[3].x), j);
+                if (st1) put(r + 1, make_float4(o[0].y, o[1].y, o[2].y, o[3].y), j);
+            }
+        });
+    }
+};
+
+template <int K>
+__device__ __forceinline__ void bandl_wave(const BandKArgs &a, int wv, int lane, float2 *park) {
+    using L = BandL<K>;
+    const int band = (wv >= a.first[1]) + (wv >= a.first[2]) + (wv >= a.first[3]);
+    const int w = wv - (band == 0 ? 0 : band == 1 ? a.first[1] : band == 2 ? a.first[2] : a.first[3]);
+    const int X = a.rows, Y = a.cols;
+    if (band < 2) {
+        // does this wave hold column 0 or Y-1 of a global left / right edge?
+        const int c_lo = w * L::SW - L::KE, c_hi = c_lo + 127;
+        const bool cp = (!a.has[2] && c_lo <= 0 && c_hi >= 0) || (!a.has[3] && c_lo <= Y - 1 && c_hi >= Y - 1);
+        if (band == 0)
+            cp ? L::template rows<false, true>(a, w, lane, park) : L::template rows<false, false>(a, w, lane, park);
+        else
+            cp ? L::template rows<true, true>(a, w, lane, park) : L::template rows<true, false>(a, w, lane, park);
+    } else {
+        const int r_lo = a.rlo + w * L::SW - L::KE, r_hi = r_lo + 127;
+        const bool cp = (!a.has[0] && r_lo <= 0 && r_hi >= 0) || (!a.has[1] && r_lo <= X - 1 && r_hi >= X - 1);
+        if (band == 2)
+            cp ? L::template cols<false, true>(a, w, lane, park) : L::template cols<false, false>(a, w, lane, park);
+        else
+            cp ? L::template cols<true, true>(a, w, lane, park) : L::template cols<true, false>(a, w, lane, park);
+    }
+}
+
+// 8 waves per EU caps the kernel at 64 VGPRs (512 / 8)
+template <int K>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void bandl_kernel(BandKArgs a) {
+    const int waves = gridDim.x * 4;
+    const int wv0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+    // band waves first: beside the interior's two waves per SIMD the bands
+    // (and the exchange behind them) finish early in the pass instead of
+    // living on the interior's leftover issue slots until its end
+    __builtin_amdgcn_s_setprio(3);
+    extern __shared__ float2 bandl_lds[];
+    float2 *park = bandl_lds + (threadIdx.x >> 6) * (BandL<K>::NPOS * 64);
+    for (int wv = wv0; wv < a.first[4]; wv += waves)  // wave-uniform
+        bandl_wave<K>(a, wv, threadIdx.x & 63, park);
+}
+
+// LDS each lean workgroup reserves: more than half of the CU's 160 KiB (its
+// four waves park 4 x NPOS x 64 float2 in it: 100 KiB at K = 20)
+constexpr int kBandLeanLds = 100 * 1024;
+static_assert(4 * BandL<SWEEPD_MAX>::NPOS * 64 * 8 <= kBandLeanLds, "lean band kernel: LDS park too small");
+
+template <int K>
+int bandl_launch_impl(const BandKArgs &a, int blocks, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+    // (once per process, thread-safe: the reservation exceeds the 64 KiB a
+    // launch may request without it)
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&bandl_kernel<K>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kBandLeanLds);
+    SMI_HIP_CHECK(attr);
+    if (start || stop)
+        hipExtLaunchKernelGGL((bandl_kernel<K>), dim3(blocks), dim3(256), kBandLeanLds, s, start, stop, 0, a);
+    else
+        hipLaunchKernelGGL((bandl_kernel<K>), dim3(blocks), dim3(256), kBandLeanLds, s, a);
+    SMI_HIP_CHECK(hipGetLastError());
+    return SMI_SUCCESS;
+}
+
 template <int K>
 int bandk_launch_impl(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
     if (start || stop)  // events carried by the dispatch itself (no marker packets around it)
@@ -270,5 +553,13 @@ int bandk_launch_impl(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t s
     int bandk_launch_k##K(const BandKArgs &a, int waves, hipStream_t s, hipEvent_t start,                \
                           hipEvent_t stop) {                                                             \
         return bandk_launch_impl<K>(a, waves, s, start, stop);                                           \
+    }                                                                                                    \
+    }
+
+#define SMI_BANDL_INSTANCE(K)                                                                            \
+    namespace smi {                                                                                      \
+    int bandl_launch_k##K(const BandKArgs &a, int blocks, hipStream_t s, hipEvent_t start,               \
+                          hipEvent_t stop) {                                                             \
+        return bandl_launch_impl<K>(a, blocks, s, start, stop);                                          \
     }                                                                                                    \
     }

@@ -1,7 +1,6 @@
 // stencil_bandk.hip -- host side of the halo-facing bands of a K-step pass
-// (kernel: stencil_bandk.h, one instantiation per K in stencilk_k<K>.hip,
-// K = 13..20 in stencild_k<K>.hip)
-// and the initial depth-K pack.
+// (kernels: stencil_bandk.h, one instantiation per K in bandk_k<K>.hip) and
+// the initial depth-K pack.
 #include <cstdlib>
 
 #include "stencil_common.h"
@@ -29,14 +28,51 @@ SMI_BANDK_DECL(18)
 SMI_BANDK_DECL(19)
 SMI_BANDK_DECL(20)
 
-int plan_bands(int K, BandKArgs *ap) {
+#define SMI_BANDL_DECL(K) \
+    int bandl_launch_k##K(const BandKArgs &a, int blocks, hipStream_t s, hipEvent_t start, hipEvent_t stop);
+SMI_BANDL_DECL(13)
+SMI_BANDL_DECL(14)
+SMI_BANDL_DECL(15)
+SMI_BANDL_DECL(16)
+SMI_BANDL_DECL(17)
+SMI_BANDL_DECL(18)
+SMI_BANDL_DECL(19)
+SMI_BANDL_DECL(20)
+
+static int compute_units() {
+    static int cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (!cached[dev]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        cached[dev] = cus;
+    }
+    return cached[dev];
+}
+
+static int launch_bandl(int K, const BandKArgs &a, int blocks, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+    switch (K) {
+    case 13: return bandl_launch_k13(a, blocks, s, start, stop);
+    case 14: return bandl_launch_k14(a, blocks, s, start, stop);
+    case 15: return bandl_launch_k15(a, blocks, s, start, stop);
+    case 16: return bandl_launch_k16(a, blocks, s, start, stop);
+    case 17: return bandl_launch_k17(a, blocks, s, start, stop);
+    case 18: return bandl_launch_k18(a, blocks, s, start, stop);
+    case 19: return bandl_launch_k19(a, blocks, s, start, stop);
+    default: return bandl_launch_k20(a, blocks, s, start, stop);
+    }
+}
+
+int plan_bands(int K, BandKArgs *ap, bool lean) {
     BandKArgs &a = *ap;
     const int X = a.rows, Y = a.cols;
     a.kc = kc_of(K);
     SMI_ARG_CHECK(K >= SWEEPK_MIN && K <= SWEEPD_MAX, "bandk: K must be 3..20");
     SMI_ARG_CHECK(X >= 2 * K && Y >= 2 * a.kc && Y % 4 == 0, "bandk: tile smaller than 2K x 2KC");
     // one wave per 64 - 2K cells along a band (stencil_bandk.h)
-    a.sw = 64 - 2 * K;
+    // lean kernel: two cells per lane, pair-aligned windows (BandL::SW)
+    a.sw = lean ? 128 - 2 * (K + (K & 1)) : 64 - 2 * K;
     a.rlo = a.has[0] ? K : 0;
     a.rhi = a.has[1] ? X - K : X;
     const int nrow = (Y + a.sw - 1) / a.sw;
@@ -56,7 +92,8 @@ int plan_bands(int K, BandKArgs *ap) {
 }
 
 int launch_bandk(int K, BandKArgs a, int max_waves, hipStream_t s, hipEvent_t stop) {
-    SMI_TRY(plan_bands(K, &a));
+    const bool lean = K >= SWEEPD_MIN && g_tune.band_lean;
+    SMI_TRY(plan_bands(K, &a, lean));
     const int segs = a.first[4];
     if (segs == 0) {
         if (stop) SMI_HIP_CHECK(hipEventRecord(stop, s));
@@ -73,6 +110,17 @@ int launch_bandk(int K, BandKArgs a, int max_waves, hipStream_t s, hipEvent_t st
         after = stop;
     }
     int rc = SMI_SUCCESS;
+    if (lean) {
+        // the lean kernel beside the interior: one workgroup (4 waves) per CU
+        // at most, fewer when max_waves asks for fewer
+        const int cus = compute_units();
+        SMI_ARG_CHECK(cus > 0, "bandl: compute-unit query failed");
+        int blocks = std::min(cus, (segs + 3) / 4);
+        if (max_waves > 0) blocks = std::min(blocks, std::max(1, max_waves / 4));
+        SMI_TRY(launch_bandl(K, a, blocks, s, start, kstop));
+        if (after) SMI_HIP_CHECK(hipEventRecord(after, s));
+        return SMI_SUCCESS;
+    }
     switch (K) {
     case 3: rc = bandk_launch_k3(a, n, s, start, kstop); break;
     case 4: rc = bandk_launch_k4(a, n, s, start, kstop); break;

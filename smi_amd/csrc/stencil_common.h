@@ -84,6 +84,10 @@ struct Tuning {
     int deep_ce16 = 10;  // tools/deep_tune.py: K = 20 at 8192^2, 0.141 ms (4/2: 0.156)
     int deep_rev16 = 6;
     int deep_waves = 0;
+    // multi-rank bands for K >= SWEEPD_MIN: 1 = the lean kernel that runs
+    // beside the interior sweep (bandl_kernel, <= 64 VGPRs, one workgroup per
+    // CU), 0 = one wave per segment (bandk_kernel)
+    int band_lean = 1;
 };
 extern Tuning g_tune;
 
@@ -196,10 +200,10 @@ struct BandKArgs {
     HaloK h;
     // filled by launch_bandk
     int first[5];      // first wave of band top, bottom, left, right; first[4] = all waves
-    int sw;            // cells stored per wave (64 - 2K)
+    int sw;            // cells stored per wave (64 - 2K; lean kernel 128 - 2 KE)
     int rlo, rhi;      // rows of the left/right bands
 };
-int plan_bands(int K, BandKArgs *a);  // fills kc, first[], sw, rlo, rhi
+int plan_bands(int K, BandKArgs *a, bool lean);  // fills kc, first[], sw, rlo, rhi
 // the bands of a pass: one wave per segment, or max_waves (> 0) waves;
 // stop (nullable): an event the launch's dispatch records at completion
 int launch_bandk(int K, BandKArgs a, int max_waves, hipStream_t s, hipEvent_t stop = nullptr);

@@ -298,6 +298,17 @@ int smi_stencil_get_bands(int *reserve_waves, int *interior_rounds) {
     return SMI_SUCCESS;
 }
 
+int smi_stencil_set_band_kernel(int lean) {
+    SMI_ARG_CHECK(lean <= 1, "band kernel: 0 (one wave per segment) or 1 (lean, beside the interior)");
+    if (lean >= 0) g_tune.band_lean = lean;
+    return SMI_SUCCESS;
+}
+
+int smi_stencil_get_band_kernel(int *lean) {
+    if (lean) *lean = g_tune.band_lean;
+    return SMI_SUCCESS;
+}
+
 int smi_stencil_set_deep(int ce16, int rev16, int waves) {
     SMI_ARG_CHECK(ce16 <= 256 && rev16 <= 256 && waves <= (1 << 20), "deep sweep settings out of range");
     if (ce16 >= 0) g_tune.deep_ce16 = ce16;

@@ -1,4 +1,3 @@
-// stencilk_k11.hip -- sweepk_kernel<11> (stencilk.h) and bandk_kernel<11> (stencil_bandk.h)
-#include "stencil_bandk.h"
+// stencilk_k11.hip -- sweepk_kernel<11> (stencilk.h)
+#include "stencilk.h"
 SMI_SWEEPK_INSTANCE(11)
-SMI_BANDK_INSTANCE(11)

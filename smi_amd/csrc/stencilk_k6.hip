@@ -1,4 +1,3 @@
-// stencilk_k6.hip -- sweepk_kernel<6> (stencilk.h) and bandk_kernel<6> (stencil_bandk.h)
-#include "stencil_bandk.h"
+// stencilk_k6.hip -- sweepk_kernel<6> (stencilk.h)
+#include "stencilk.h"
 SMI_SWEEPK_INSTANCE(6)
-SMI_BANDK_INSTANCE(6)

@@ -1,4 +1,3 @@
-// stencilk_k8.hip -- sweepk_kernel<8> (stencilk.h) and bandk_kernel<8> (stencil_bandk.h)
-#include "stencil_bandk.h"
+// stencilk_k8.hip -- sweepk_kernel<8> (stencilk.h)
+#include "stencilk.h"
 SMI_SWEEPK_INSTANCE(8)
-SMI_BANDK_INSTANCE(8)

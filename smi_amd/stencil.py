@@ -81,7 +81,7 @@ def run(comm: Comm, tile: torch.Tensor, timesteps: int, PX: int, PY: int,
     X, Y = tile.shape
     idx = ctypes.c_int()
     _lib.call("smi_stencil_run", comm.handle, tile.data_ptr(), scratch.data_ptr(), X, Y, PX, PY,
-              timesteps, _lib.stream_handle(stream), ctypes.byref(idx))
+              timesteps, _lib.stream_handle(stream, tile.get_device()), ctypes.byref(idx))
     return tile if idx.value == 0 else scratch
 
 
@@ -141,6 +141,18 @@ def get_fusion() -> dict:
     v = [ctypes.c_int() for _ in range(3)]
     _lib.call("smi_stencil_get_fusion", *[ctypes.byref(x) for x in v])
     return dict(steps_per_pass=v[0].value, rows_per_wave=v[1].value, rows_in_flight=v[2].value)
+
+
+def set_band_kernel(lean: int = -1) -> None:
+    """Multi-rank K >= 13 band kernel (bit-neutral): 1 = lean, beside the
+    interior sweep (default); 0 = one wave per segment.  -1 keeps it."""
+    _lib.call("smi_stencil_set_band_kernel", lean)
+
+
+def get_band_kernel() -> int:
+    v = ctypes.c_int()
+    _lib.call("smi_stencil_get_band_kernel", ctypes.byref(v))
+    return v.value
 
 
 def set_deep(ce16: int = -1, rev16: int = -1, waves: int = -1) -> None:

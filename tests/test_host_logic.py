@@ -175,6 +175,26 @@ def test_band_settings_roundtrip_and_validate():
         stencil.set_bands(old["reserve_waves"], old["interior_rounds"])
 
 
+def test_band_kernel_setting_roundtrip_and_validate():
+    """smi_stencil_set_band_kernel: 1 = the lean band kernel beside the
+    interior (default), 0 = one wave per segment; -1 keeps it, anything else
+    is refused."""
+    from smi_amd import stencil
+    from smi_amd._lib import SMIError
+    old = stencil.get_band_kernel()
+    assert old == 1  # default (DESIGN.md §6)
+    try:
+        stencil.set_band_kernel(0)
+        assert stencil.get_band_kernel() == 0
+        stencil.set_band_kernel(-1)
+        assert stencil.get_band_kernel() == 0
+        with pytest.raises(SMIError):
+            stencil.set_band_kernel(2)
+        assert stencil.get_band_kernel() == 0
+    finally:
+        stencil.set_band_kernel(old)
+
+
 # ------------------------------------------------------ gloo, world_size 2 --
 def _free_port():
     s = socket.socket()

@@ -468,10 +468,12 @@ def test_ring_decomposed(gpu, oracle_mod, k, pxpy, overlap):
 
 
 @pytest.mark.parametrize("k", [16, 20])
-@pytest.mark.parametrize("bands", [(0, 1), (64, 1), (500, 1)])
+@pytest.mark.parametrize("bands", [(0, 1), (4, 1), (64, 1), (500, 1)])
 def test_ring_band_reserve_is_bit_neutral(gpu, oracle_mod, k, bands):
     """Wave slots reserved for the band kernel come off the rotating-ring
-    interior's round of waves: scheduling only."""
+    interior's round of waves and cap the lean band kernel's grid (4: one
+    workgroup whose four waves walk every segment in turn): scheduling
+    only."""
     from smi_amd import stencil
     old = stencil.get_bands()
     stencil.set_bands(*bands)
@@ -482,6 +484,28 @@ def test_ring_band_reserve_is_bit_neutral(gpu, oracle_mod, k, bands):
             assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, k + 1))), (k, bands, overlap)
     finally:
         stencil.set_bands(old["reserve_waves"], old["interior_rounds"])
+
+
+@pytest.mark.parametrize("k", [13, 14, 17, 20])
+@pytest.mark.parametrize("pxpy", [(1, 2), (2, 1), (3, 3), (2, 4)])
+def test_band_kernel_choice_is_bit_neutral(gpu, oracle_mod, k, pxpy):
+    """The lean band kernel (bandl_kernel: KS = ceil(K/7) staged walks through
+    LDS, <= 64 VGPRs, one workgroup per CU) and the one-wave-per-segment
+    kernel (bandk_kernel) give the same bits, both equal to the oracle;
+    global edges on every side of some rank (the copy rule inside the band
+    walks), tiles 137 x 268 (ragged band segments)."""
+    from smi_amd import stencil
+    PX, PY = pxpy
+    g = oracle_mod.init_uniform(137 * PX, 268 * PY, seed=k * 7 + PX * 3 + PY)
+    want = bits(oracle_mod.stencil(g, k + 2))
+    old = stencil.get_band_kernel()
+    try:
+        for lean in (1, 0):
+            stencil.set_band_kernel(lean)
+            got = _run_fused(g, k + 2, PX, PY, 1, k=k)
+            assert np.array_equal(bits(got), want), (k, pxpy, lean)
+    finally:
+        stencil.set_band_kernel(old)
 
 
 def test_ring_full_size_8192_driver_config(gpu, oracle_mod):

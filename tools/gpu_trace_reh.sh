@@ -12,7 +12,7 @@ for spec in "$@"; do
   name=${spec%%:*}
   envs=${spec#*:}
   echo "=== $name ($envs)"
-  env $envs REHEARSAL_PROF=0 REHEARSAL_OVERLAP=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$name -o run -- python $R/tools/rehearsal.py 8192 12 > $O/trace_$name.log 2>&1
+  env $envs REHEARSAL_PROF=0 REHEARSAL_OVERLAP=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$name -o run -- python $R/tools/rehearsal.py 8192 ${REH_K:-12} > $O/trace_$name.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "=== FAILED rc=$rc"; tail -5 $O/trace_$name.log; exit $rc; fi
   grep '^{' $O/trace_$name.log

@@ -17,7 +17,8 @@ def main():
     with open(path) as f:
         for r in csv.DictReader(f):
             name = r["Kernel_Name"]
-            kind = ("interior" if "sweepk_kernel" in name or "sweepk_fused_kernel" in name else "band" if "bandk_kernel" in name or "ringk" in name
+            kind = ("interior" if "sweepk_kernel" in name or "sweepd_kernel" in name or "sweepk_fused_kernel" in name
+                    else "band" if "bandk_kernel" in name or "bandl_kernel" in name or "ringk" in name
                     else "xchg" if "copy" in name.lower() or "nccl" in name.lower() else None)
             if kind:
                 ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind))
@@ -28,11 +29,30 @@ def main():
     for s, e, k in ev:
         if s >= t0 - 200_000:
             print(f"{k:9s} {(s - t0) / 1e3:10.1f} {(e - t0) / 1e3:10.1f} {(e - s) / 1e3:8.1f}")
+    # each band / exchange launch against the interior it ran beside (the
+    # one whose span contains its start): inside = it also ended before
+    # that interior did
+    import json
+    rows = []
+    for s, e, k in ev:
+        if k == "interior" or s < t0:
+            continue
+        host = next((i for i in ints if i[0] <= s <= i[1]), None)
+        rows.append((k, host is not None and e <= host[1], (e - host[1]) / 1e3 if host else None))
+    summ = {}
+    for k in ("band", "xchg"):
+        r = [x for x in rows if x[0] == k]
+        if r:
+            summ[k] = {"launches": len(r), "inside_interior": sum(1 for x in r if x[1]),
+                       "max_overhang_us": round(max((x[2] for x in r if x[2] is not None), default=0.0), 1)}
     if len(ints) > 1:
         last = ints[-n:]
         per = (last[-1][1] - last[0][0]) / len(last) / 1e3
         print(f"interior pass period over the last {len(last)}: {per:.1f} us; "
               f"interior duration avg {sum(e - s for s, e, _ in last) / len(last) / 1e3:.1f} us")
+        summ["interior"] = {"period_us": round(per, 1),
+                            "duration_avg_us": round(sum(e - s for s, e, _ in last) / len(last) / 1e3, 1)}
+    print(json.dumps(summ))
 
 
 if __name__ == "__main__":

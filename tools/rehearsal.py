@@ -13,7 +13,9 @@ single-tile run, i.e. an estimate of per-GPU weak-scaling efficiency with
 an exchange that costs one device-to-device copy of the halo bytes.
 REHEARSAL_ROUNDS (list) sets the rounds of resident waves the multi-rank
 interior sweep is cut into, REHEARSAL_RESERVE (list) the wave slots it leaves
-free for the band kernel and the exchange (smi_stencil_set_bands).
+free for the band kernel and the exchange (smi_stencil_set_bands),
+REHEARSAL_LEAN (list, default 1) the band kernel for K >= 13 (1 = the lean
+kernel beside the interior, 0 = one wave per segment).
 REHEARSAL_PROF=0 times the runs without the library's profiling markers (the
 band / interior averages are then not reported).
 SMI_LOOPBACK_FUSED=1 prices the exchange as one copy kernel (like one RCCL
@@ -70,8 +72,11 @@ def main():
         noxchg = os.environ.get("SMI_LOOPBACK_NOXCHG")
         grid = [(r, b) for r in (int(x) for x in os.environ.get("REHEARSAL_ROUNDS", "1,2,3").split(","))
                 for b in (int(x) for x in os.environ.get("REHEARSAL_RESERVE", "0").split(","))]
-        for rounds, reserve in grid:
+        grid = [(r, b, lean) for r, b in grid
+                for lean in (int(x) for x in os.environ.get("REHEARSAL_LEAN", "1").split(","))]
+        for rounds, reserve, lean in grid:
             stencil.set_bands(reserve, rounds)
+            stencil.set_band_kernel(lean)
             for ov in [int(x) for x in os.environ.get("REHEARSAL_OVERLAP", "1,0").split(",")]:
                 stencil.set_tuning(overlap=ov)
                 # the lone tile right before each setting (the GPU clock
@@ -85,7 +90,7 @@ def main():
                 band = profiling.read(profiling.EDGE)
                 sweep = profiling.read(profiling.SWEEPK if k >= 4 else profiling.SWEEP)
                 os.environ.pop("SMI_LOOPBACK", None)
-                print(json.dumps({"K": k, "rounds": rounds, "reserve_waves": reserve, "no_bands": bool(os.environ.get("SMI_REH_NOBANDS")), "prof": os.environ.get("REHEARSAL_PROF", "1") != "0", "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
+                print(json.dumps({"K": k, "rounds": rounds, "reserve_waves": reserve, "band_kernel": "lean" if lean and k >= 13 else "wave per segment", "no_bands": bool(os.environ.get("SMI_REH_NOBANDS")), "prof": os.environ.get("REHEARSAL_PROF", "1") != "0", "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
                                   "ms_per_step_alone": round(alone, 5),
                                   "ms_per_step_interior_rank": round(loop, 5),
                                   "efficiency": round(alone / loop, 4),
@@ -94,6 +99,7 @@ def main():
                                   "interior_avg_ms": round(sweep[0] / max(sweep[1], 1), 5)}), flush=True)
     stencil.set_tuning(overlap=1)
     stencil.set_bands(0, 1)
+    stencil.set_band_kernel(1)
     comm.finalize()
 
 
