@@ -72,15 +72,22 @@ int sweepd_geometry(int K, const SweepKArgs &a, int reserve, SweepDGeom *g) {
     if (reserve > 0) waves = std::max(64, waves - reserve);
     int nrb = std::max(1, (int)((long)waves * 16 / ((long)r.n_int * 16 + (long)nce * ce16)));
     const bool both = a.gT && a.gB;
+    // every block at least K rows (the shortest is a weighted bottom block)
+    auto shortest = [&](const SweepDGeom &q) {
+        const int nbmax = nce ? q.nrb_ce : q.nrb;
+        const long den = (long)(nbmax - 1) * 16 + (a.gB ? q.wlast : 16);
+        return (long)out_rows * std::min(16, a.gB ? q.wlast : 16) / den;
+    };
     for (;; --nrb) {
         r.nrb = std::max(nrb, both ? 2 : 1);
         r.nrb_ce = std::max(r.nrb, r.nrb * ce16 / 16);
-        const int nbmax = nce ? r.nrb_ce : r.nrb;
-        // every block at least K rows (the shortest is a weighted bottom block)
-        const long den = (long)(nbmax - 1) * 16 + (a.gB ? r.wlast : 16);
-        const long hmin = (long)out_rows * std::min(16, a.gB ? r.wlast : 16) / den;
-        if (hmin - 1 >= K || nrb <= (both ? 2 : 1)) {
-            SMI_ARG_CHECK(hmin - 1 >= K, "sweepd: tile too short for this K");
+        if (shortest(r) - 1 >= K) break;
+        if (nrb <= (both ? 2 : 1)) {
+            // a short tile (down to 4K rows, sweepd_fits): no balancing
+            // weights, every strip in the same equal blocks
+            r.nrb_ce = r.nrb;
+            r.wlast = 16;
+            SMI_ARG_CHECK(shortest(r) - 1 >= K, "sweepd: tile too short for this K");
             break;
         }
     }
