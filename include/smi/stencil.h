@@ -115,6 +115,16 @@ int smi_stencil_get_band_kernel(int *lean);
 int smi_stencil_set_deep(int ce16, int rev16, int waves);
 int smi_stencil_get_deep(int *ce16, int *rev16, int *waves);
 
+/* The rotating-ring sweep's work split for one K-step pass (K = 13..20) of a
+ * rows x cols tile whose sides with a neighbour are set in side_mask (bit 0
+ * top, 1 bottom, 2 left, 3 right; the sweep then covers the tile minus K rows
+ * / KC columns there, as in smi_stencil_run): waves launched, column strips,
+ * row blocks per interior strip and per edge-column strip, and the output
+ * rows of the shortest block (every block must exceed K).  Host only; with
+ * no device, set the launch's waves first (smi_stencil_set_deep). */
+int smi_stencil_deep_geometry(int rows, int cols, int K, int side_mask, int *waves, int *strips, int *row_blocks,
+                              int *row_blocks_edge, int *min_block_rows);
+
 /* One phase of a planned run: `passes` launches of `steps_per_pass` steps. */
 typedef struct {
     int steps_per_pass;

@@ -68,6 +68,7 @@ SIGNATURES = {
     "smi_stencil_set_band_kernel": (I, [I]),
     "smi_stencil_get_band_kernel": (I, [ctypes.POINTER(I)]),
     "smi_stencil_set_deep": (I, [I, I, I]),
+    "smi_stencil_deep_geometry": (I, [I, I, I, I] + [ctypes.POINTER(I)] * 5),
     "smi_stencil_get_deep": (I, [ctypes.POINTER(I)] * 3),
     "smi_reduce": (I, [SMI_Comm, P, P, SZ, I, I, I, I, P]),
     "smi_reduce_fold": (I, [P, P, I, SZ, SZ, I, I, P]),

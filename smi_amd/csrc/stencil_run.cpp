@@ -324,6 +324,43 @@ int smi_stencil_get_deep(int *ce16, int *rev16, int *waves) {
     return SMI_SUCCESS;
 }
 
+int smi_stencil_deep_geometry(int rows, int cols, int K, int side_mask, int *waves, int *strips, int *row_blocks,
+                              int *row_blocks_edge, int *min_block_rows) {
+    SMI_ARG_CHECK(rows >= 1 && cols >= 4 && cols % 4 == 0, "tile must be >= 1 x 4, cols % 4 == 0");
+    SMI_ARG_CHECK(side_mask >= 0 && side_mask < 16, "side_mask: bits 0..3");
+    SweepKArgs a{};
+    a.rows = rows;
+    a.cols = cols;
+    const int kc = kc_of(K);
+    a.row_lo = (side_mask & 1) ? K : 0;
+    a.row_hi = (side_mask & 2) ? rows - K : rows;
+    a.col_lo = (side_mask & 4) ? kc : 0;
+    a.col_hi = (side_mask & 8) ? cols - kc : cols;
+    a.gT = !(side_mask & 1);
+    a.gB = !(side_mask & 2);
+    a.gL = !(side_mask & 4);
+    a.gR = !(side_mask & 8);
+    SMI_ARG_CHECK(sweepd_fits(K, a), "K outside 13..20 or sweep rectangle shorter than 4K rows");
+    SweepDGeom g;
+    SMI_TRY(sweepd_geometry(K, a, 0, &g));
+    int hmin = rows;
+    for (int pass = 0; pass < 2; ++pass) {
+        const int nb = pass ? g.nrb_ce : g.nrb;
+        if (pass ? (g.tasks == g.n_int * g.nrb) : g.n_int == 0) continue;
+        for (int rb = 0; rb < nb; ++rb) {
+            int o0, o1;
+            sweepd_block_rows(a, rb, nb, g.wlast, &o0, &o1);
+            hmin = std::min(hmin, o1 - o0);
+        }
+    }
+    if (waves) *waves = g.tasks;
+    if (strips) *strips = g.nstrips;
+    if (row_blocks) *row_blocks = g.nrb;
+    if (row_blocks_edge) *row_blocks_edge = g.tasks == g.n_int * g.nrb ? 0 : g.nrb_ce;
+    if (min_block_rows) *min_block_rows = hmin;
+    return SMI_SUCCESS;
+}
+
 int smi_stencil_plan(int x_local, int y_local, int px, int py, int rank, int timesteps, SMI_StencilPhase *phases,
                      int max_phases, int *nphases, int *neighbours, int *result_index) {
     SMI_ARG_CHECK(x_local >= 1 && y_local >= 4 && y_local % 4 == 0, "tile must be >= 1 x 4, y_local % 4 == 0");

@@ -155,6 +155,15 @@ def get_band_kernel() -> int:
     return v.value
 
 
+def deep_geometry(rows: int, cols: int, k: int, side_mask: int = 0) -> dict:
+    """The rotating-ring sweep's work split for one K-step pass (host only;
+    with no device set the launch's waves first: set_deep(waves=...))."""
+    v = [ctypes.c_int() for _ in range(5)]
+    _lib.call("smi_stencil_deep_geometry", rows, cols, k, side_mask, *[ctypes.byref(x) for x in v])
+    return dict(waves=v[0].value, strips=v[1].value, row_blocks=v[2].value, row_blocks_edge=v[3].value,
+                min_block_rows=v[4].value)
+
+
 def set_deep(ce16: int = -1, rev16: int = -1, waves: int = -1) -> None:
     """Rotating-ring sweep (K = 13..20) geometry, scheduling only: extra work
     of edge-column strips / upward bottom blocks in 16ths, waves per launch

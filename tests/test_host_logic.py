@@ -195,6 +195,38 @@ def test_band_kernel_setting_roundtrip_and_validate():
         stencil.set_band_kernel(old)
 
 
+@pytest.mark.parametrize("waves", [1024, 2048, 3072])
+def test_deep_geometry_every_block_holds_k_rows(waves):
+    """sweepd_geometry (smi_stencil_deep_geometry, host only) over every K =
+    13..20, every side mask and sweep rectangles from the 4K-row minimum up:
+    it never fails on a rectangle sweepd_fits admits and every row block is
+    at least K rows (the triangular prologue needs K rows per block) -- the
+    balancing weights are dropped on short tiles.  Launch sizes of 1, 2 and
+    3 resident waves per SIMD."""
+    from smi_amd import stencil
+    old = stencil.get_deep()
+    stencil.set_deep(waves=waves)
+    try:
+        for k in range(13, 21):
+            kc = 4 * ((k + 3) // 4)
+            for mask in range(16):
+                top, bot, left, right = (mask >> 0) & 1, (mask >> 1) & 1, (mask >> 2) & 1, (mask >> 3) & 1
+                for rect in (4 * k, 4 * k + 1, 5 * k + 3, 8 * k, 300, 1000, 8192):
+                    rows = rect + k * (top + bot)
+                    for cols in (8, 64, 136, 264, 1028, 8192):
+                        if cols - kc * (left + right) < 8:
+                            continue
+                        g = stencil.deep_geometry(rows, cols, k, mask)
+                        assert g["min_block_rows"] >= k, (k, mask, rows, cols, g)
+                        assert g["waves"] >= g["strips"] >= 1, (k, mask, rows, cols, g)
+        with pytest.raises(Exception):
+            stencil.deep_geometry(4 * 13 - 1, 264, 13, 0)  # shorter than 4K rows
+        with pytest.raises(Exception):
+            stencil.deep_geometry(8192, 8192, 12, 0)  # not a rotating-ring K
+    finally:
+        stencil.set_deep(old["ce16"], old["rev16"], old["waves"])
+
+
 # ------------------------------------------------------ gloo, world_size 2 --
 def _free_port():
     s = socket.socket()
