@@ -76,14 +76,40 @@ def lib_path(variant: str = "") -> str:
     return os.path.join(OUT_DIR, variant, f"libsmi_amd_{variant}.so")
 
 
+def _lib_deps() -> list[str]:
+    return sorted(sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(
+        os.path.join(ROOT, "include", "**", "*.h"), recursive=True))
+
+
+def _src_hash(variant: str = "") -> str:
+    """Content hash of every source and header the library is built from,
+    with the build flags."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(" ".join(CXXFLAGS + VARIANT_FLAGS[variant] + [f"{k}={v}" for k, v in sorted(FILE_FLAGS.items())]).encode())
+    for d in _lib_deps():
+        h.update(os.path.relpath(d, ROOT).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def _stale(variant: str = "") -> bool:
+    """The library is stale when a source or header is newer than it AND the
+    sources' content differs from what it was built from (a copied tree --
+    the GPU box's snapshot, a checkout -- may carry newer mtimes for the same
+    content: rebuilding there would take many minutes for nothing)."""
     lib = lib_path(variant)
     if not os.path.exists(lib):
         return True
     t = os.path.getmtime(lib)
-    deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(
-        os.path.join(ROOT, "include", "**", "*.h"), recursive=True)
-    return any(os.path.getmtime(d) > t for d in deps)
+    if not any(os.path.getmtime(d) > t for d in _lib_deps()):
+        return False
+    try:
+        with open(lib + ".srchash") as f:
+            return f.read().strip() != _src_hash(variant)
+    except OSError:
+        return True
 
 
 def _deps(src: str, seen: set | None = None) -> set:
@@ -157,6 +183,8 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     tmp = lib + ".tmp"
     subprocess.run([hipcc, *objs, *LDFLAGS, f"--offload-arch={ARCH}", "-o", tmp], check=True)
     os.replace(tmp, lib)
+    with open(lib + ".srchash", "w") as f:
+        f.write(_src_hash(variant) + "\n")
     return lib
 
 

@@ -443,15 +443,15 @@ struct BandL {
             g1r[J] = ldg(J, pa1, pb1);
         };
         fetch(std::integral_constant<int, E0 / 4>{});
-        if constexpr (E0 / 4 + 1 < G4) fetch(std::integral_constant<int, E0 / 4 + 1>{});
         auto comp = [](const float4 &q4, int e) { return e == 0 ? q4.x : e == 1 ? q4.y : e == 2 ? q4.z : q4.w; };
         walk<false, CP, NC, L0>(
             cpa, cpb,
             [&](auto T) {
                 constexpr int t = T, e = E0 + t;
-                // entering group e/4: fetch the one after the next
+                // entering group e/4: fetch the next (two rows x 4 floats
+                // per group in flight: the 64-VGPR budget)
                 if constexpr (e % 4 == 0 || t == 0)
-                    if constexpr (e / 4 + 2 < G4) fetch(std::integral_constant<int, e / 4 + 2>{});
+                    if constexpr (e / 4 + 1 < G4) fetch(std::integral_constant<int, e / 4 + 1>{});
                 return make_float2(comp(g0r[e / 4], e % 4), comp(g1r[e / 4], e % 4));
             },
             [&](auto U, float2 v) { park[U * 64 + lane] = v; });
