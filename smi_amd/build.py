@@ -86,7 +86,8 @@ def _src_hash(variant: str = "") -> str:
     with the build flags."""
     import hashlib
     h = hashlib.sha256()
-    h.update(" ".join(CXXFLAGS + VARIANT_FLAGS[variant] + [f"{k}={v}" for k, v in sorted(FILE_FLAGS.items())]).encode())
+    flags = " ".join(CXXFLAGS + VARIANT_FLAGS[variant] + [f"{k}={v}" for k, v in sorted(FILE_FLAGS.items())])
+    h.update(flags.replace(ROOT, "<root>").encode())  # the same tree anywhere on disk
     for d in _lib_deps():
         h.update(os.path.relpath(d, ROOT).encode())
         with open(d, "rb") as f:

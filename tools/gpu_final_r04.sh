@@ -4,6 +4,10 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 T=$1
+# a fresh box pages the image in at the first import torch (1-2 min without
+# output): once, printing around it, before pytest's quiet collection
+echo "=== warm"
+timeout -k 10 300 python -u -c 'print("importing torch", flush=True); import torch; print("torch", flush=True); torch.zeros(1).cuda(); import smi_amd; smi_amd.load(build_if_missing=False); print("warm", flush=True)' || exit 1
 bash tools/gpu_tests.sh $T || exit $?
 TESTS=none bash tools/gpu_r04.sh $T || exit $?
 O=gpurun_out/$T
