@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 import torch  # noqa: F401  (see module docstring)
 
@@ -110,10 +111,19 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     if _lib is not None:
         return _lib
     path = lib_path()
-    if not os.path.exists(path) or (build_if_missing and _build._stale(variant())):
+    if not os.path.exists(path):
         if not build_if_missing:
             raise SMIError(f"{path} missing: run smi_amd.build.build()")
         _build.build(variant=variant())
+    elif build_if_missing and _build._stale(variant()):
+        # Rebuild where the library is built (no GPU here); on a GPU host
+        # (the library travels there prebuilt) a rebuild takes many minutes
+        # inside a test or a bench: load what is there and say so.
+        if torch.cuda.device_count() > 0:  # counts devices without initialising HIP
+            sys.stderr.write(f"[smi_amd] {path} is older than its sources; loading it anyway "
+                             "(rebuild with python smi_amd/build.py)\n")
+        else:
+            _build.build(variant=variant())
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in list(SIGNATURES.items()):
         fn = getattr(lib, name)
