@@ -23,8 +23,9 @@ HBM before the timed region; the timed region is exactly K steps bracketed by
 a barrier + device synchronize on both sides; the time is the max over ranks.
 
 A run of T steps is planned as ceil(T / 20) sweep passes of at most 20 steps
-(single tile; passes of more than 12 steps run the rotating-ring sweep,
-stencild.h; multi-rank runs use at most 12), balanced to within one step
+(passes of more than 12 steps run the rotating-ring sweep, stencild.h, on
+single tiles and on multi-rank interiors alike; a tile too small for a deep
+pass -- fewer than 4K rows in its sweep rectangle -- clips K to 12), balanced to within one step
 when T % 20 >= 3 (config.plan; the driver's 20 steps are one pass).  Before the timed
 region every kernel of that plan launches once and untimed runs of the same
 plan repeat for at least --warmup-ms (GPU clock settling; with N > 1 every rank
@@ -159,7 +160,10 @@ def cpu_baseline(budget_s: float = 2.0) -> dict:
     restatement (the reference's own CPU path -- Intel FPGA emulator + MPI --
     cannot be built here or on the box):
       value       -- the stencil on every host thread this job may use
-                     (OpenMP), 8192^2 tile, chunks of 4 steps for ~budget_s;
+                     (OpenMP), 8192^2 tile stepped in place between two
+                     preallocated buffers for ~budget_s (no allocation in
+                     the timed calls); legs.all_affinity_cpus: the same on
+                     every CPU of the affinity mask when that is more;
       legs.serial_reference_order -- the host Reference() loop order
                      (examples/host/stencil_smi.cpp:33-46) on 1 core;
       legs.emulator_config1 / emulator_2x4 -- the rank-decomposed program
@@ -173,23 +177,41 @@ def cpu_baseline(budget_s: float = 2.0) -> dict:
     cpu = host_cpu()
     threads = cpu["threads"]
     g = oracle.init_uniform(TILE, TILE, seed=42)
-    state = {"g": g}
+    # two preallocated, first-touched buffers stepped in place: the timed
+    # calls allocate nothing (round 4 timed a malloc + first touch of 768 MiB
+    # per 4-step chunk and understated the CPU by ~3.7x)
+    bufs = (g, np.empty_like(g))
 
-    def omp_chunk():
-        state["g"] = oracle.stencil(state["g"], 4, threads=threads)
+    def rate(thr: int, budget: float) -> tuple[float, int, float]:
+        oracle.stencil_steps(bufs[0], bufs[1], 2, threads=thr)  # warm: pages, thread pool
+        chunk, steps, dt = 4, 0, 0.0
+        while dt < budget:
+            t0 = time.perf_counter()
+            oracle.stencil_steps(bufs[0], bufs[1], chunk, threads=thr)  # even: result back in bufs[0]
+            dt += time.perf_counter() - t0
+            steps += chunk
+            chunk = min(chunk * 2, 64)
+        return TILE * TILE * steps / dt / 1e9, steps, dt
 
-    reps, dt = _time_loop(omp_chunk, budget_s)
-    steps = 4 * reps
+    value, steps, dt = rate(threads, budget_s)
     out = {
-        "value": round(TILE * TILE * steps / dt / 1e9, 3),
+        "value": round(value, 3),
         "unit": "GCell/s",
         "cores": threads,
         "kind": "port",
         "sample": f"{TILE}x{TILE} fp32 Jacobi, {steps} steps, OpenMP C restatement "
-                  f"(oracle/smi_oracle.c) of stencil_smi.cl:117-165, {dt:.1f} s wall on {threads} threads",
+                  f"(oracle/smi_oracle.c oracle_stencil_steps: two preallocated buffers stepped in place) "
+                  f"of stencil_smi.cl:117-165, {dt:.1f} s wall on {threads} threads "
+                  f"(this job's CPU share; all {cpu['affinity_cpus']} affinity CPUs in legs)",
         **cpu,
     }
     legs = {}
+    if cpu["affinity_cpus"] != threads:
+        v_all, st_all, dt_all = rate(cpu["affinity_cpus"], min(1.0, budget_s))
+        legs["all_affinity_cpus"] = {"GCells": round(v_all, 3), "cores": cpu["affinity_cpus"],
+                                     "sample": f"{st_all} steps in {dt_all:.2f} s on every CPU of the "
+                                               f"affinity mask (beyond this job's share: contended)"}
+    del bufs
     gs = g[:2048, :2048].copy()
     reps, dt = _time_loop(lambda: oracle.stencil(gs, 2, order="host", threads=1), 1.5)
     legs["serial_reference_order"] = {
@@ -915,6 +937,9 @@ def main() -> None:
             "fake_host": bool(os.environ.get("SMI_BENCH_FAKE_HOST")),
             "warmup_ms_floor": args.warmup_ms,
             "warmup_ms_run": round(warm_ms, 1),
+            # the library's recorded source hash; load() refuses a library whose
+            # hash differs from this tree's (smi_amd.build._src_hash())
+            "lib_srchash": smi_amd._lib.recorded_srchash(),
         },
         "roofline": {
             "bound": "hbm",

@@ -70,6 +70,7 @@ def lib() -> ctypes.CDLL:
         I = ctypes.c_int
         _lib.oracle_stencil.argtypes = [P, P, I, I, I, I, I]
         _lib.oracle_stencil_decomposed.argtypes = [P, P, I, I, I, I, I, I]
+        _lib.oracle_stencil_steps.argtypes = [P, P, I, I, I, I]
         _lib.oracle_reduce.argtypes = [P, P, I, ctypes.c_long, I, I, P, I]
         _lib.oracle_bcast.argtypes = [P, I, I, ctypes.c_long, I]
         _lib.oracle_gesummv.argtypes = [P, P, P, P, I, I, ctypes.c_float, ctypes.c_float, I]
@@ -80,7 +81,7 @@ def lib() -> ctypes.CDLL:
         _lib.oracle_kmeans_reference_data.argtypes = [I, I, I, P, P, P]
         _lib.oracle_minstd_rand0_10000.argtypes = []
         _lib.oracle_minstd_rand0_10000.restype = ctypes.c_ulong
-        for f in ("oracle_stencil", "oracle_stencil_decomposed", "oracle_reduce", "oracle_bcast",
+        for f in ("oracle_stencil", "oracle_stencil_decomposed", "oracle_stencil_steps", "oracle_reduce", "oracle_bcast",
                   "oracle_gesummv", "oracle_max_threads", "oracle_kmeans_assign",
                   "oracle_kmeans_accumulate", "oracle_kmeans", "oracle_kmeans_reference_data"):
             getattr(_lib, f).restype = ctypes.c_int
@@ -108,17 +109,35 @@ def init_uniform(X: int, Y: int, seed: int = 42) -> np.ndarray:
     return rng.random((X, Y), dtype=np.float32)
 
 
+STENCIL_ORDERS = {"device": 0, "host": 1, "tree": 2}
+
+
 def stencil(grid: np.ndarray, T: int, order: str = "device", threads: int = 0) -> np.ndarray:
     """T Jacobi steps.  order='device' is the stencil_smi.cl:153-156 order
     (S+W+E+N); order='host' is the reference host Reference() order
-    (N+S+W+E, stencil_smi.cpp:33-46)."""
+    (N+S+W+E, stencil_smi.cpp:33-46); order='tree' is the balanced tree
+    (S+W)+(E+N) an -fp-relaxed build may reassociate the device order into
+    (CMakeLists.txt:70,188) -- test-only, to quantify that divergence."""
     g = np.ascontiguousarray(grid, dtype=np.float32)
     out = np.empty_like(g)
     X, Y = g.shape
-    rc = lib().oracle_stencil(_ptr(g), _ptr(out), X, Y, T, 0 if order == "device" else 1, threads)
+    rc = lib().oracle_stencil(_ptr(g), _ptr(out), X, Y, T, STENCIL_ORDERS[order], threads)
     if rc:
         raise ValueError(f"oracle_stencil rc={rc}")
     return out
+
+
+def stencil_steps(a: np.ndarray, b: np.ndarray, T: int, threads: int = 0) -> np.ndarray:
+    """T device-order steps ping-ponging between two preallocated C-contiguous
+    float32 buffers (a holds the input; both are overwritten).  Returns the
+    buffer holding the result.  No allocation inside: bench.py times this."""
+    assert a.flags.c_contiguous and b.flags.c_contiguous and a.shape == b.shape
+    assert a.dtype == np.float32 and b.dtype == np.float32
+    X, Y = a.shape
+    rc = lib().oracle_stencil_steps(_ptr(a), _ptr(b), X, Y, T, threads)
+    if rc < 0:
+        raise ValueError(f"oracle_stencil_steps rc={rc}")
+    return b if rc else a
 
 
 def stencil_decomposed(grid: np.ndarray, T: int, PX: int, PY: int, threads: int = 1) -> np.ndarray:

@@ -60,7 +60,10 @@ static inline float cell_device(float s, float w, float e, float n) {
     float sum = s + w;
     sum = sum + e;
     sum = sum + n;
-    return (float)(0.25 * (double)sum);
+    /* == (float)(0.25 * (double)sum): the double product is exact and is
+     * rounded to float once, as the float product is (also in the subnormal
+     * range); the float form lets the compiler vectorize the row */
+    return 0.25f * sum;
 }
 
 /* The reference host's Reference() order: 0.25f * (N + S + W + E)
@@ -72,9 +75,19 @@ static inline float cell_host(float s, float w, float e, float n) {
     return 0.25f * sum;
 }
 
+/* TEST-ONLY (not a reference order): the balanced tree (S+W)+(E+N) that the
+ * emulator's -fp-relaxed build (/root/reference/CMakeLists.txt:66-73, applied
+ * to every target at :188) would be allowed to form by reassociating
+ * stencil_smi.cl:153-156.  tests/test_oracle.py quantifies how far it lands
+ * from the source order; the GPU is held to the source order. */
+static inline float cell_tree(float s, float w, float e, float n) {
+    return 0.25f * ((s + w) + (e + n));
+}
+
 /* One full-grid Jacobi step with global-edge cells copied unchanged
  * (stencil_smi.cl:143-151 for the device, stencil_smi.cpp:36-37 for the
- * host).  order: 0 = device (S+W+E+N), 1 = host Reference (N+S+W+E). */
+ * host).  order: 0 = device (S+W+E+N), 1 = host Reference (N+S+W+E),
+ * 2 = the test-only balanced tree (S+W)+(E+N). */
 static void jacobi_step(const float *in, float *out, int X, int Y, int order) {
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < X; ++i) {
@@ -90,9 +103,12 @@ static void jacobi_step(const float *in, float *out, int X, int Y, int order) {
         if (order == 0) {
             for (int j = 1; j < Y - 1; ++j)
                 o[j] = cell_device(s[j], c[j - 1], c[j + 1], n[j]);
-        } else {
+        } else if (order == 1) {
             for (int j = 1; j < Y - 1; ++j)
                 o[j] = cell_host(s[j], c[j - 1], c[j + 1], n[j]);
+        } else {
+            for (int j = 1; j < Y - 1; ++j)
+                o[j] = cell_tree(s[j], c[j - 1], c[j + 1], n[j]);
         }
         if (Y > 1) o[Y - 1] = c[Y - 1];
     }
@@ -122,6 +138,27 @@ int oracle_stencil(const float *in, float *out, int X, int Y, int T, int order,
     free(a);
     free(b);
     return 0;
+}
+
+/* T device-order Jacobi steps ping-ponging between two caller-owned buffers
+ * (a holds the input): no allocation or first touch inside, so a timed run
+ * measures the stepping alone (bench.py cpu_baseline; the reference host
+ * steps its two halves in place the same way, stencil_smi.cpp:33-46).
+ * Returns 0 when the result is in a, 1 when in b, < 0 on bad arguments. */
+int oracle_stencil_steps(float *a, float *b, int X, int Y, int T, int threads) {
+    if (X <= 0 || Y <= 0 || T < 0 || !a || !b) return -1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+    for (int t = 0; t < T; ++t) {
+        if (t & 1)
+            jacobi_step(b, a, X, Y, 0);
+        else
+            jacobi_step(a, b, X, Y, 0);
+    }
+    return T & 1;
 }
 
 /* Rank-decomposed restatement of the stencil_smi emulator program:

@@ -105,25 +105,45 @@ def lib_path() -> str:
     return _build.lib_path(variant())
 
 
+def recorded_srchash(path: str | None = None) -> str | None:
+    """The source hash recorded beside the library when it was linked
+    (smi_amd.build writes <lib>.srchash), or None."""
+    try:
+        with open((path or lib_path()) + ".srchash") as f:
+            return f.read().strip() or None
+    except OSError:
+        return None
+
+
+def verify_fresh(path: str | None = None) -> str:
+    """Raise SMIError unless the library at `path` was built from exactly the
+    sources, headers and flags of this tree (content hash, not mtimes);
+    returns the hash."""
+    path = path or lib_path()
+    want = _build._src_hash(variant())
+    got = recorded_srchash(path)
+    if got != want:
+        raise SMIError(f"{path} was not built from these sources (recorded source hash "
+                       f"{(got or 'missing')[:16]}, tree {want[:16]}): rebuild with python smi_amd/build.py "
+                       f"on the build host")
+    return want
+
+
 def load(build_if_missing: bool = True) -> ctypes.CDLL:
-    """Load (building first if needed and allowed) libsmi_amd.so."""
+    """Load libsmi_amd.so, refusing a library that was not built from this
+    tree's sources.  A missing or stale library is (re)built only where it is
+    built -- a host without a GPU -- and only if build_if_missing; on a GPU
+    host (the library travels there prebuilt) a stale library raises."""
     global _lib
     if _lib is not None:
         return _lib
     path = lib_path()
-    if not os.path.exists(path):
-        if not build_if_missing:
-            raise SMIError(f"{path} missing: run smi_amd.build.build()")
-        _build.build(variant=variant())
-    elif build_if_missing and _build._stale(variant()):
-        # Rebuild where the library is built (no GPU here); on a GPU host
-        # (the library travels there prebuilt) a rebuild takes many minutes
-        # inside a test or a bench: load what is there and say so.
-        if torch.cuda.device_count() > 0:  # counts devices without initialising HIP
-            sys.stderr.write(f"[smi_amd] {path} is older than its sources; loading it anyway "
-                             "(rebuild with python smi_amd/build.py)\n")
-        else:
+    if not os.path.exists(path) or recorded_srchash(path) != _build._src_hash(variant()):
+        if build_if_missing and torch.cuda.device_count() == 0:  # counts devices without initialising HIP
             _build.build(variant=variant())
+        elif not os.path.exists(path):
+            raise SMIError(f"{path} missing: run python smi_amd/build.py on the build host")
+    verify_fresh(path)
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in list(SIGNATURES.items()):
         fn = getattr(lib, name)

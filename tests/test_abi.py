@@ -94,3 +94,30 @@ def test_c_header_compiles_standalone(tmp_path):
                     f"-L{libdir}", "-lsmi_amd", f"-Wl,-rpath,{libdir}"], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True)
     assert out.stdout.split()[0] == "1"
+
+
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """A library whose recorded source hash differs from this tree's is never
+    loaded: a copy with a tampered .srchash raises, on a
+    GPU host and on the build host alike (the mtimes say "fresh", so nothing
+    rebuilds it), and the untampered copy passes."""
+    import shutil
+
+    from smi_amd import _lib
+    src = _lib.lib_path()
+    _lib.load()  # the real library is fresh
+    dst = tmp_path / "libsmi_amd.so"
+    shutil.copy(src, dst)
+    shutil.copy(src + ".srchash", str(dst) + ".srchash")
+    assert _lib.verify_fresh(str(dst)) == _lib._build._src_hash()
+    (tmp_path / "libsmi_amd.so.srchash").write_text("0" * 64 + "\n")
+    with pytest.raises(_lib.SMIError, match="not built from these sources"):
+        _lib.verify_fresh(str(dst))
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "lib_path", lambda: str(dst))
+    for bim in (False, True):
+        with pytest.raises(_lib.SMIError, match="not built from these sources"):
+            _lib.load(build_if_missing=bim)
+    (tmp_path / "libsmi_amd.so.srchash").unlink()
+    with pytest.raises(_lib.SMIError, match="missing"):
+        _lib.load(build_if_missing=False)

@@ -389,8 +389,8 @@ def test_deep_decomposed_small_tiles(gpu, oracle_mod, k):
 
 
 # ------------------------- K = 13..20 steps per pass (rotating-ring sweep) --
-# stencild.h: single tiles only (multi-rank runs clip K to 12); tiles shorter
-# than 4K rows clip K to 12 too.
+# stencild.h: single tiles and multi-rank interiors (beside bandk_kernel /
+# bandl_kernel<K>); a sweep rectangle shorter than 4K rows clips K to 12.
 RING_SHAPES = [(52, 8), (80, 260), (129, 500), (300, 1028), (1000, 516), (257, 2060), (96, 4)]
 
 
