@@ -31,6 +31,45 @@ __global__ __launch_bounds__(256) void multicopy_kernel(CopySegs c, int nseg) {
         dst[i] = src[i];
 }
 
+#ifdef SMI_LOOPBACK_REHEARSAL
+// Rehearsal only: the same copies with the resource footprint of RCCL's
+// rcclGenericKernel<4> on gfx950 (tools/rccl_footprint.py: 280 VGPRs incl.
+// 32 AGPRs, 256-thread workgroups, 19,744 B of LDS), so that the exchange
+// finds wave slots beside the interior sweep exactly as RCCL's kernel would.
+// `blocks` plays RCCL's channel count; every block walks every segment.
+__global__ __launch_bounds__(256) void heavycopy_kernel(CopySegs c, int nseg) {
+    __shared__ uint4 lds[19744 / 16];
+    asm volatile("; rccl footprint" ::: "v247", "a31");  // 248 + 32 = 280 registers, as rcclGenericKernel<4>
+    lds[threadIdx.x] = make_uint4(threadIdx.x, 0, 0, 0);
+    __syncthreads();
+    const unsigned long long stride = (unsigned long long)gridDim.x * 256;
+    for (int seg = 0; seg < nseg; ++seg) {
+        const uint4 *src = c.src[seg];
+        uint4 *dst = c.dst[seg];
+        for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < c.n16[seg]; i += stride)
+            dst[i] = src[i];
+    }
+    if (lds[(threadIdx.x + 1) & 255].x == 0xffffffffu) c.dst[0][0] = make_uint4(0, 0, 0, 0);  // keeps the LDS
+}
+
+int launch_heavy_copies(const void *const *src, void *const *dst, const size_t *bytes, int n, int blocks,
+                        hipStream_t s) {
+    CopySegs c{};
+    int nseg = 0;
+    for (int i = 0; i < n && nseg < kCopyMaxSegs; ++i) {
+        if (bytes[i] == 0) continue;
+        if (((uintptr_t)src[i] & 15u) || ((uintptr_t)dst[i] & 15u) || bytes[i] % 16) return SMI_ERR_INVALID_ARG;
+        c.src[nseg] = reinterpret_cast<const uint4 *>(src[i]);
+        c.dst[nseg] = reinterpret_cast<uint4 *>(dst[i]);
+        c.n16[nseg] = bytes[i] / 16;
+        ++nseg;
+    }
+    hipLaunchKernelGGL(heavycopy_kernel, dim3(std::max(1, blocks)), dim3(256), 0, s, c, nseg);
+    SMI_HIP_CHECK(hipGetLastError());
+    return SMI_SUCCESS;
+}
+#endif
+
 int launch_copies(const void *const *src, void *const *dst, const size_t *bytes, int n, hipStream_t s) {
     CopySegs c{};
     int nseg = 0, blocks = 0;

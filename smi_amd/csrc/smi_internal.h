@@ -150,5 +150,9 @@ size_t type_size(int type);
 // Device-to-device copies in one kernel launch (copy.hip); segments that are
 // not 16-byte aligned multiples go through hipMemcpyAsync.
 int launch_copies(const void *const *src, void *const *dst, const size_t *bytes, int n, hipStream_t s);
+#ifdef SMI_LOOPBACK_REHEARSAL
+int launch_heavy_copies(const void *const *src, void *const *dst, const size_t *bytes, int n, int blocks,
+                        hipStream_t s);
+#endif
 
 }  // namespace smi

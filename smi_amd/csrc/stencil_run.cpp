@@ -134,6 +134,17 @@ static int exchangek(Comm *c, const Neighbours &nb, const float *tile, int rows,
         const size_t by[8] = {rb, rb, cb, cb, kb, kb, kb, kb};
         return launch_copies(src, dst, by, 8, s);
     }
+    if (const char *hv = getenv("SMI_LOOPBACK_HEAVY")) {
+        if (nb.top == 0 && nb.left == 0 && nb.tl == 0) {
+            // rehearsal: one copy kernel with rcclGenericKernel's footprint,
+            // SMI_LOOPBACK_HEAVY workgroups (RCCL's channels)
+            const void *src[8] = {tile, tile + (size_t)(rows - K) * cols, h.send_left, h.send_right,
+                                  h.send_corner[0], h.send_corner[1], h.send_corner[2], h.send_corner[3]};
+            void *dst[8] = {h.bot, h.top, h.right, h.left, h.corner[3], h.corner[2], h.corner[1], h.corner[0]};
+            const size_t by[8] = {rb, rb, cb, cb, kb, kb, kb, kb};
+            return launch_heavy_copies(src, dst, by, 8, atoi(hv), s);
+        }
+    }
 #endif
     Group grp(tp);
     SMI_TRY(grp.begin(s));

@@ -19,7 +19,7 @@ def main():
             name = r["Kernel_Name"]
             kind = ("interior" if "sweepk_kernel" in name or "sweepd_kernel" in name or "sweepk_fused_kernel" in name
                     else "band" if "bandk_kernel" in name or "bandl_kernel" in name or "ringk" in name
-                    else "xchg" if "copy" in name.lower() or "nccl" in name.lower() else None)
+                    else "xchg" if "copy" in name.lower() or "nccl" in name.lower() or "rccl" in name.lower() else None)
             if kind:
                 ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind))
     ev.sort()

@@ -19,7 +19,12 @@ kernel beside the interior, 0 = one wave per segment).
 REHEARSAL_PROF=0 times the runs without the library's profiling markers (the
 band / interior averages are then not reported).
 SMI_LOOPBACK_FUSED=1 prices the exchange as one copy kernel (like one RCCL
-group), SMI_LOOPBACK_NOXCHG=1 leaves it out.
+group), SMI_LOOPBACK_NOXCHG=1 leaves it out, SMI_LOOPBACK_HEAVY=<blocks> as
+one copy kernel of that many 256-thread workgroups with rcclGenericKernel's
+register and LDS footprint (280 VGPRs, 19.7 KB; tools/rccl_footprint.py).
+REHEARSAL_TRANSPORT=rccl runs the exchange through the real RCCL kernel: a
+one-rank RCCL communicator whose 8 sends and receives go to itself (RCCL's
+self send/recv, one group per pass, the production RcclTransport).
 usage: rehearsal.py [tile] [K...]
 """
 import json
@@ -57,11 +62,26 @@ def _timed(comm, t, sc, steps):
     return dt / steps * 1e3
 
 
+def exchange_label(noxchg) -> str:
+    if noxchg:
+        return "none"
+    if os.environ.get("SMI_LOOPBACK_FUSED"):
+        return "one copy kernel"
+    if os.environ.get("SMI_LOOPBACK_HEAVY"):
+        return f"one copy kernel with rcclGenericKernel's footprint, {os.environ['SMI_LOOPBACK_HEAVY']} workgroups"
+    if os.environ.get("REHEARSAL_TRANSPORT") == "rccl":
+        return "RCCL self send/recv (one-rank communicator, rcclGenericKernel)"
+    return "in-process transport"
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
     ks = [int(k) for k in sys.argv[2:]] or [12]
     smi_amd.load(build_if_missing=False)
-    comm = smi_amd.LocalGroup(1).comm(0)
+    if os.environ.get("REHEARSAL_TRANSPORT") == "rccl":
+        comm = smi_amd.Comm.create(0, 1, 0, smi_amd.Comm.unique_id())
+    else:
+        comm = smi_amd.LocalGroup(1).comm(0)
     t = torch.rand((n, n), device="cuda")
     sc = torch.empty_like(t)
     for k in ks:
@@ -90,7 +110,7 @@ def main():
                 band = profiling.read(profiling.EDGE)
                 sweep = profiling.read(profiling.SWEEPK if k >= 4 else profiling.SWEEP)
                 os.environ.pop("SMI_LOOPBACK", None)
-                print(json.dumps({"K": k, "rounds": rounds, "reserve_waves": reserve, "band_kernel": "lean" if lean and k >= 13 else "wave per segment", "no_bands": bool(os.environ.get("SMI_REH_NOBANDS")), "prof": os.environ.get("REHEARSAL_PROF", "1") != "0", "overlap": ov, "tile": n, "exchange": "none" if noxchg else ("one copy kernel" if os.environ.get("SMI_LOOPBACK_FUSED") else "transport"),
+                print(json.dumps({"K": k, "rounds": rounds, "reserve_waves": reserve, "band_kernel": "lean" if lean and k >= 13 else "wave per segment", "no_bands": bool(os.environ.get("SMI_REH_NOBANDS")), "prof": os.environ.get("REHEARSAL_PROF", "1") != "0", "overlap": ov, "tile": n, "exchange": exchange_label(noxchg),
                                   "ms_per_step_alone": round(alone, 5),
                                   "ms_per_step_interior_rank": round(loop, 5),
                                   "efficiency": round(alone / loop, 4),
