@@ -189,6 +189,37 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     return lib
 
 
+HOSTS_DIR = os.path.join(ROOT, "hosts")
+
+
+def build_hosts(force: bool = False, verbose: bool = False) -> list[str]:
+    """Compile the C++ host programs (hosts/*.cpp: the reference host programs
+    restated on the C ABI) against include/ and the release libsmi_amd.so into
+    hosts/_build/, linked with an $ORIGIN-relative rpath so they run from any
+    copy of the tree (the GPU box's snapshot included)."""
+    lib = build()
+    out_dir = os.path.join(HOSTS_DIR, "_build")
+    os.makedirs(out_dir, exist_ok=True)
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    outs = []
+    for src in sorted(glob.glob(os.path.join(HOSTS_DIR, "*.cpp"))):
+        exe = os.path.join(out_dir, os.path.splitext(os.path.basename(src))[0])
+        outs.append(exe)
+        if not force and os.path.exists(exe) and os.path.getmtime(exe) >= max(
+                os.path.getmtime(src), os.path.getmtime(lib)):
+            continue
+        cmd = [hipcc, "-O2", "-std=c++17", "-Wall", f"-I{os.path.join(ROOT, 'include')}", src, "-o", exe,
+               f"-L{OUT_DIR}", "-lsmi_amd", "-lpthread", "-Wl,-rpath,$ORIGIN/../../smi_amd/_build",
+               f"-Wl,-rpath,{ROCM}/lib"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+    return outs
+
+
 if __name__ == "__main__":
+    if "--hosts" in sys.argv:
+        print("\n".join(build_hosts(force="--force" in sys.argv, verbose=True)))
+        sys.exit(0)
     v = next((a[2:] for a in sys.argv[1:] if a.startswith("--") and a[2:] in VARIANT_FLAGS), "")
     print(build(force="--force" in sys.argv, verbose=True, variant=v))
