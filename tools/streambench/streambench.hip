@@ -34,6 +34,30 @@ __global__ void small_kernel(float *out, int iters) {
     if (v == -1.0f) out[threadIdx.x] = v;
 }
 
+// mode 13: the big kernel's waves wait on a device flag instead of a
+// cross-stream wait packet; the band stand-in's last block releases it
+__global__ void copy_wait_kernel(const float4 *__restrict__ in, float4 *__restrict__ out, size_t n,
+                                 const unsigned *flag, unsigned target) {
+    if (threadIdx.x == 0) {
+        while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target)
+            __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
+__global__ void small_flag_kernel(float *out, int iters, unsigned *count, unsigned *flag, unsigned value) {
+    float v = threadIdx.x;
+    for (int i = 0; i < iters; ++i) v = v * 1.0000001f + 0.5f;
+    if (v == -1.0f) out[threadIdx.x] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned done = __hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
+        if (done == value * gridDim.x) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 struct Ctx {
     float4 *a, *b;
     size_t n;
@@ -41,6 +65,7 @@ struct Ctx {
     hipStream_t s, cs;
     hipEvent_t e_int, e_band;
     uint32_t *f_int, *f_band;  // hipMallocSignalMemory counters (mode 7)
+    unsigned *dflag, *dcount;  // device flag + block counter (mode 13)
     static constexpr int kPool = 4096;
     hipEvent_t pool[kPool];
 };
@@ -75,8 +100,16 @@ static void small_ev(Ctx &c, hipStream_t st, hipEvent_t stop) {
 // was enqueued, or a later one?
 // 10 / 11: as 2 / 8 with the main kernel's completion event carried by its
 // dispatch (hipExtLaunchKernelGGL) instead of a record packet
+// 12: one stream, the big kernel launched with hipExtAnyOrderLaunch after the
+// small one; 13: no wait packet on the main stream: the big kernel's blocks
+// wait on a device flag the small kernel's last block releases (round 5)
 static double run(Ctx &c, int mode, int passes) {
     CK(hipDeviceSynchronize());
+    if (mode == 13) {
+        CK(hipMemset(c.dflag, 0, 4));
+        CK(hipMemset(c.dcount, 0, 4));
+        CK(hipDeviceSynchronize());
+    }
     if (mode == 7) {  // counters restart at 0 (nothing pending on them now)
         CK(hipStreamWriteValue32(c.s, c.f_int, 0u, 0));
         CK(hipStreamWriteValue32(c.s, c.f_band, 0u, 0));
@@ -127,6 +160,20 @@ static double run(Ctx &c, int mode, int passes) {
             CK(hipStreamWriteValue32(c.s, c.f_int, (uint32_t)(p + 1), 0));
             CK(hipStreamWaitValue32(c.s, c.f_band, (uint32_t)(p + 1), hipStreamWaitValueGte, 0xFFFFFFFFu));
             CK(hipStreamWaitValue32(c.cs, c.f_int, (uint32_t)(p + 1), hipStreamWaitValueGte, 0xFFFFFFFFu));
+        } else if (mode == 12) {
+            // one stream: the band stand-in, then the big kernel launched
+            // with hipExtAnyOrderLaunch (no barrier bit: may it overlap?)
+            small(c, c.s);
+            hipExtLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, c.s, nullptr, nullptr, hipExtAnyOrderLaunch,
+                                  p & 1 ? c.b : c.a, p & 1 ? c.a : c.b, c.n);
+        } else if (mode == 13) {
+            // cs: [wait big(t-1)] band(t) -> flag = t + 1 (its last block);
+            // s: big(t) back to back, its blocks wait for flag >= t (band(t-1))
+            if (p > 0) CK(hipStreamWaitEvent(c.cs, c.e_int, 0));
+            hipLaunchKernelGGL(small_flag_kernel, dim3(800), dim3(64), 0, c.cs, c.sink, 2000, c.dcount, c.dflag,
+                               (unsigned)(p + 1));
+            hipExtLaunchKernelGGL(copy_wait_kernel, dim3(4096), dim3(256), 0, c.s, nullptr, c.e_int, 0,
+                                  p & 1 ? c.b : c.a, p & 1 ? c.a : c.b, c.n, (const unsigned *)c.dflag, (unsigned)p);
         } else if (mode == 3) {
             small(c, c.s);
             big(c, p);
@@ -152,6 +199,8 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&c.a, c.n * 16));
     CK(hipMalloc(&c.b, c.n * 16));
     CK(hipMalloc(&c.sink, 4096));
+    CK(hipMalloc(&c.dflag, 256));
+    CK(hipMalloc(&c.dcount, 256));
     CK(hipMemset(c.a, 0, c.n * 16));
     int can_wait = 0;
     CK(hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, 0));
@@ -170,7 +219,7 @@ int main(int argc, char **argv) {
             CK(hipStreamCreateWithPriority(&c.cs, hipStreamNonBlocking, prio ? greatest : least));
             CK(hipEventCreateWithFlags(&c.e_int, evflags[ef]));
             CK(hipEventCreateWithFlags(&c.e_band, evflags[ef]));
-            for (int mode = 0; mode < 12; mode += (mode == 2 ? 6 : 1)) {
+            for (int mode = 0; mode < 14; mode += (mode == 2 ? 6 : 1)) {
                 run(c, mode, 20);  // warm-up
                 const double us = run(c, mode, passes);
                 printf("{\"mode\": %d, \"comm_prio\": \"%s\", \"events\": \"%s\", \"us_per_pass\": %.2f}\n", mode,
