@@ -40,11 +40,17 @@ import smi_amd  # noqa: E402
 from smi_amd import profiling, stencil  # noqa: E402
 
 
+LAST_CHRONO = []
+
+
 def timed(comm, t, sc, steps, reps=5):
     """ms per step of `reps` runs, sorted (the in-process transport creates
     and retires HIP events per message: occasional host stalls that RCCL
-    does not have, so the min is the estimate)"""
-    return sorted(_timed(comm, t, sc, steps) for _ in range(reps))
+    does not have, so the min is the estimate); LAST_CHRONO keeps the same
+    runs in the order they ran"""
+    runs = [_timed(comm, t, sc, steps) for _ in range(reps)]
+    LAST_CHRONO[:] = runs
+    return sorted(runs)
 
 
 def _timed(comm, t, sc, steps):
@@ -115,6 +121,8 @@ def main():
                                   "ms_per_step_interior_rank": round(loop, 5),
                                   "efficiency": round(alone / loop, 4),
                                   "runs_ms_per_step": [round(r, 5) for r in runs],
+                                  "runs_chronological": [round(r, 5) for r in LAST_CHRONO],
+                                  "efficiency_median": round(alone / runs[len(runs) // 2], 4),
                                   "band_avg_ms": round(band[0] / max(band[1], 1), 5),
                                   "interior_avg_ms": round(sweep[0] / max(sweep[1], 1), 5)}), flush=True)
     stencil.set_tuning(overlap=1)

@@ -80,8 +80,8 @@ static void small_long(Ctx &c, hipStream_t st) {
     hipLaunchKernelGGL(small_kernel, dim3(16), dim3(64), 0, st, c.sink, 3000);
 }
 // the same launches with the completion event carried by the dispatch itself
-static void big_ev(Ctx &c, int p, hipEvent_t stop) {
-    hipExtLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, c.s, nullptr, stop, 0, p & 1 ? c.b : c.a,
+static void big_ev(Ctx &c, int p, hipEvent_t stop, hipStream_t st = nullptr) {
+    hipExtLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, st ? st : c.s, nullptr, stop, 0, p & 1 ? c.b : c.a,
                           p & 1 ? c.a : c.b, c.n);
 }
 static void small_ev(Ctx &c, hipStream_t st, hipEvent_t stop) {
@@ -103,6 +103,8 @@ static void small_ev(Ctx &c, hipStream_t st, hipEvent_t stop) {
 // 12: one stream, the big kernel launched with hipExtAnyOrderLaunch after the
 // small one; 13: no wait packet on the main stream: the big kernel's blocks
 // wait on a device flag the small kernel's last block releases (round 5)
+// 14 / 15: the streams swap roles every pass so that the wait before each
+// big kernel is armed while its predecessor still runs (round 5)
 static double run(Ctx &c, int mode, int passes) {
     CK(hipDeviceSynchronize());
     if (mode == 13) {
@@ -174,6 +176,16 @@ static double run(Ctx &c, int mode, int passes) {
                                (unsigned)(p + 1));
             hipExtLaunchKernelGGL(copy_wait_kernel, dim3(4096), dim3(256), 0, c.s, nullptr, c.e_int, 0,
                                   p & 1 ? c.b : c.a, p & 1 ? c.a : c.b, c.n, (const unsigned *)c.dflag, (unsigned)p);
+        } else if (mode == 14 || mode == 15) {
+            // streams swap roles every pass: big(p) on A = (p even ? s : cs),
+            // small(p) on B after big(p-1) by queue order (big(p-1) ran on B),
+            // then B waits for big(p) -- a wait armed long before big(p) ends
+            // -- and runs big(p + 1).  15: the same with the long small kernel.
+            hipStream_t A = (p & 1) ? c.cs : c.s, B = (p & 1) ? c.s : c.cs;
+            if (p == 0) big_ev(c, p, c.pool[0], A);  // big(0) on A
+            if (mode == 14) small(c, B); else small_long(c, B);
+            CK(hipStreamWaitEvent(B, c.pool[p % kPool], 0));  // big(p) done
+            big_ev(c, p + 1, c.pool[(p + 1) % kPool], B);   // big(p + 1), on B
         } else if (mode == 3) {
             small(c, c.s);
             big(c, p);
@@ -219,7 +231,7 @@ int main(int argc, char **argv) {
             CK(hipStreamCreateWithPriority(&c.cs, hipStreamNonBlocking, prio ? greatest : least));
             CK(hipEventCreateWithFlags(&c.e_int, evflags[ef]));
             CK(hipEventCreateWithFlags(&c.e_band, evflags[ef]));
-            for (int mode = 0; mode < 14; mode += (mode == 2 ? 6 : 1)) {
+            for (int mode = 0; mode < 16; mode += (mode == 2 ? 6 : 1)) {
                 run(c, mode, 20);  // warm-up
                 const double us = run(c, mode, passes);
                 printf("{\"mode\": %d, \"comm_prio\": \"%s\", \"events\": \"%s\", \"us_per_pass\": %.2f}\n", mode,
