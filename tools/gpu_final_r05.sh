@@ -12,8 +12,8 @@ O=gpurun_out/$T; mkdir -p $O
 step() { echo "=== $1"; shift; "$@"; rc=$?; if [ $rc -ne 0 ]; then echo "=== FAILED rc=$rc"; exit $rc; fi; }
 echo "=== warm"
 timeout -k 10 300 python -u -c 'print("importing torch", flush=True); import torch; torch.zeros(1).cuda(); import smi_amd; smi_amd.load(build_if_missing=False); print("warm", flush=True)' || exit 1
-step tests bash tools/gpu_tests.sh $T
-step bench TESTS=none PROF=1 bash tools/gpu_r04.sh $T
+[ -n "$SKIP_TESTS" ] || step tests bash tools/gpu_tests.sh $T
+step bench env TESTS=none PROF=1 bash tools/gpu_r04.sh $T
 bash tools/gpu_prof_r04.sh $T/prof > $O/prof.log 2>&1 || { tail -5 $O/prof.log; exit 1; }
 G="REHEARSAL_PASSES=20 REHEARSAL_ROUNDS=1 REHEARSAL_RESERVE=0 REHEARSAL_LEAN=1 REHEARSAL_OVERLAP=1 REHEARSAL_PROF=0"
 for spec in rccl:REHEARSAL_TRANSPORT=rccl heavy16:SMI_LOOPBACK_HEAVY=16 transport:; do
