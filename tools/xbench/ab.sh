@@ -15,7 +15,7 @@ python3 - $out/ab.jsonl <<'PY'
 import json, sys, collections
 res = collections.defaultdict(list)
 for l in open(sys.argv[1]):
-    d = json.loads(l); res[(d["variant"], d["kernel"], d.get("wcone"))].append((d["ms_med"], d["ms_min"], d["mismatches"]))
+    d = json.loads(l); res[(d["variant"], d["kernel"], d.get("wcone"), d.get("fo"))].append((d["ms_med"], d["ms_min"], d["mismatches"]))
 for k, v in res.items():
     print(k, "med", sorted(x[0] for x in v), "min", min(x[1] for x in v), "mismatches", max(x[2] for x in v))
 PY

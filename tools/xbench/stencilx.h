@@ -116,6 +116,7 @@ struct SweepX {
     int wv, ps;          // my wave and my partner's in the workgroup
     int r_out, r_in;     // rounds published / consumed
     int lane;
+    int prio_phase;  // SMI_X_PRIO_ROWS experiment
     float4 R[N];
 
     static constexpr int ph(int p, int j) { return ((p - j) % N + N) % N; }
@@ -295,17 +296,68 @@ struct SweepX {
         if constexpr (TC == K + 1) store_row<REV, SC>(t, v);
     }
 
+    // Level l of the row at rotation J (steady state): v = new_{l-1} in, new_l out.
+    template <bool REV, int CE, bool SC, int J, int l>
+    __device__ __forceinline__ void level(float4 &v) {
+        constexpr int ia = ph(D + 2 * l, J), ib = ph(D + 2 * l - 1, J);
+        float4 nv = step<REV, CE, SC>(R[ia], R[ib], v);
+        if constexpr (l < K) R[ia] = nv;
+        v = nv;
+    }
+
+    // Steady-state rows t and t + 1 (rotations J, J + 1), their level chains
+    // interleaved one level apart (stencild.h SweepD::pair): row t + 1's
+    // level l - 1 needs row t's level l - 2 only, so each pair of level
+    // steps is independent -- twice the independent work per wave.
+    template <bool REV, int CE, bool SC, int J>
+    __device__ __forceinline__ void pairrows(int t) {
+        R[ph(0, J)] = ld<REV>(min(t + D, n_in - 1));
+        float4 va = R[ph(D, J)];
+        float4 vb = R[ph(D, J + 1)];
+        if constexpr (SC) {
+            note(va);
+            note(vb);
+        }
+        level<REV, CE, SC, J, 1>(va);
+        static_for<K - 1>([&](auto L) {
+            constexpr int l = L + 2;
+            level<REV, CE, SC, J, l>(va);
+            level<REV, CE, SC, (J + 1) % N, l - 1>(vb);
+        });
+        store_row<REV, SC>(t, va);
+        R[ph(0, J + 1)] = ld<REV>(min(t + 1 + D, n_in - 1));
+        level<REV, CE, SC, (J + 1) % N, K>(vb);
+        store_row<REV, SC>(t + 1, vb);
+    }
+
     // rows t + r .. t + N - 1 of one loop body (stencild.h SweepD::body)
     template <bool REV, int CE, bool SC, int r>
     __device__ __forceinline__ bool body(int t) {
         if constexpr (r == N) {
             return true;
         } else {
+#ifdef SMI_X_PAIRROWS
+            static_assert(N % 2 == 0 && G == 2, "pairs of rows need an even cycle");
+            if (t + r >= n_in) return false;
+            pairrows<REV, CE, SC, (J0 + r) % N>(t + r);
+            return body<REV, CE, SC, r + 2>(t);
+#else
             if constexpr (r % G == 0) {
                 if (t + r >= n_in) return false;
+#ifdef SMI_X_PRIO_ROWS
+                // experiment: the two waves of a SIMD trade the VALU issue
+                // priority every SMI_X_PRIO_ROWS rows, in opposite phase
+                // (otherwise the older wave wins every arbitration and the
+                // younger one finishes alone, at the one-wave issue rate)
+                if ((((t + r) / SMI_X_PRIO_ROWS) + prio_phase) & 1)
+                    __builtin_amdgcn_s_setprio(1);
+                else
+                    __builtin_amdgcn_s_setprio(0);
+#endif
             }
             row<REV, CE, SC, (J0 + r) % N, -1>(t + r);
             return body<REV, CE, SC, r + 1>(t);
+#endif
         }
     }
 
@@ -373,6 +425,11 @@ struct SweepX {
 // workgroup holds one band of two neighbouring strips and an XCD's
 // contiguous workgroups hold whole row bands: the strips' overlapping
 // window columns meet in its L2.
+#ifdef SMI_X_WAVETIMES
+// experiment: per wave, its hardware place and its start / end shader clock
+__device__ unsigned long long *g_wavetimes;
+#endif
+
 template <int K>
 __device__ __forceinline__ void sweepx_wave(const SweepKArgs &a, const SweepXGeom &g, SweepXShared *sh, int gb,
                                             int wv, int lane) {
@@ -404,6 +461,12 @@ __device__ __forceinline__ void sweepx_wave(const SweepKArgs &a, const SweepXGeo
     w.ps = wv ^ 1;
     w.r_out = w.r_in = 0;
     w.lane = lane;
+#if defined(SMI_X_PRIO_BLOCK)
+    w.prio_phase = __builtin_amdgcn_readfirstlane((int)(blockIdx.x >> 8) & 1);
+#else
+    // HW_ID bits [3:0]: this wave's slot on its SIMD (s_getreg hwreg(HW_REG_HW_ID, 0, 4))
+    w.prio_phase = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4) & 1);
+#endif
     sweepx_block_rows(a.row_lo, a.row_hi, b, nbs, g.wcone, &w.o0, &w.o1);
 #ifdef SMI_X_NOPAIR
     const bool paired = false;
@@ -454,10 +517,119 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMI_X_WPE, 
     }
     __syncthreads();
     if (gb < g.tasks) {
+#ifdef SMI_X_WAVETIMES
+        const unsigned long long t0 = __builtin_readcyclecounter();
+#endif
         sweepx_wave<K>(a, g, &sh, gb, wv, lane);
+#ifdef SMI_X_WAVETIMES
+        const unsigned long long t1 = __builtin_readcyclecounter();
+        if (lane == 0) {
+            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);    // HW_REG_HW_ID
+            const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID
+            g_wavetimes[3 * gb + 0] = ((unsigned long long)xcc << 32) | hw;
+            g_wavetimes[3 * gb + 1] = t0;
+            g_wavetimes[3 * gb + 2] = t1;
+        }
+#endif
     } else {
         __syncthreads();  // the guard's barrier of the workgroup's walking waves
     }
 }
+
+// ---------------------------------------------------------------------------
+// Experiment (SMI_X_UNEQUAL): the library's sweepd walk with unequal halves.
+// With two waves per SIMD the older one (blockIdx < P: the first workgroup on
+// every CU) issues at the one-wave rate and the younger one takes what is
+// left, so equal blocks leave the younger wave walking alone for the last
+// third of the pass (xbench_x20t wavetimes).  Here block pairs (2j, 2j+1) of
+// the library geometry are one pair task: workgroup b < P (old) walks the top
+// fo/256 of the pair's output rows, workgroup b + P (young) the rest.
+#ifdef SMI_X_UNEQUAL
+template <int K>
+__device__ __forceinline__ void sweepu_task(const SweepKArgs &a, int strip, int o0, int o1, int lane) {
+    using S = SweepD<K>;
+    constexpr int SW = 256 - 2 * S::KC;
+    S w;
+    w.in = a.in;
+    w.out = a.out;
+    w.rows = a.rows;
+    w.cols = a.cols;
+    w.o0 = o0;
+    w.o1 = o1;
+    w.n_in = (w.o1 - w.o0) + 2 * K;
+    const int cs = (a.col_lo & ~31) + strip * SW;
+    const int cb = cs - S::KC + 4 * lane;
+    w.voff_ld = min(max(cb, 0), a.cols - 4) * 4;
+    const bool st = lane >= S::LL && lane < 64 - S::LL && cb >= a.col_lo && cb < a.col_hi;
+    w.row_bytes = a.cols * 4;
+    w.voff = st ? cb * 4 : 0x7ffffff0;
+    w.maskL = __builtin_amdgcn_ballot_w64(a.gL && cb == 0);
+    w.maskR = __builtin_amdgcn_ballot_w64(a.gR && cb + 4 == a.cols);
+    w.quarter = f32x2{0.25f, 0.25f};
+    const int ce = ((a.gL && cs - S::KC <= 0) ? 1 : 0) | ((a.gR && cs - S::KC + 256 >= a.cols) ? 2 : 0);
+    const bool top = a.gT && w.o0 == 0;
+    const bool bot = a.gB && w.o1 == a.rows;
+    const bool rev = bot && !top;
+    w.maskE = __builtin_amdgcn_ballot_w64(top || bot);
+    w.r_begin = rev ? w.o1 - 1 + K : w.o0 - K;
+    switch ((rev ? 2 : 0) + (ce ? 1 : 0)) {
+    case 0: w.template go<false, 0>(); break;
+    case 1: w.template go<false, 3>(); break;
+    case 2: w.template go<true, 0>(); break;
+    default: w.template go<true, 3>(); break;
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) void sweepu_kernel(SweepKArgs a,
+                                                                                                 SweepDGeom g,
+                                                                                                 int P, int fo) {
+    const int b = blockIdx.x;
+    const int gen = b >= P ? 1 : 0;
+    const int lp = xcd_remap(b - gen * P, P);
+    const int lane = threadIdx.x & 63;
+    const int pair = __builtin_amdgcn_readfirstlane(lp * 4 + (int)(threadIdx.x >> 6));
+    const int pi = g.n_int * (g.nrb >> 1);
+    if (pair >= (g.tasks >> 1)) return;
+    int strip, rb, nb;
+    if (pair < pi) {
+        const int rp = pair / g.n_int;
+        strip = g.int0 + pair - rp * g.n_int;
+        rb = 2 * rp;
+        nb = g.nrb;
+    } else {
+        const int t2 = pair - pi, h = g.nrb_ce >> 1;
+        const int k = t2 / h;
+        strip = g.ce[k];
+        rb = 2 * (t2 - k * h);
+        nb = g.nrb_ce;
+    }
+    int o0, o1, x0, x1;
+    sweepd_block_rows(a, rb, nb, g.wlast, &o0, &x0);
+    sweepd_block_rows(a, rb + 1, nb, g.wlast, &x1, &o1);
+    const int om = o0 + (int)((long)(o1 - o0) * fo / 256);
+#ifdef SMI_X_WAVETIMES
+    const unsigned long long t0 = __builtin_readcyclecounter();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (gen == 0) sweepu_task<K>(a, strip, o0, om, lane);
+    else sweepu_task<K>(a, strip, om, o1, lane);
+#ifdef SMI_X_WAVETIMES
+    const unsigned long long t1 = __builtin_readcyclecounter();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+        // shader clock cycles and 100 MHz real time of the walk
+        const int gb = 2 * pair + gen;
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+        const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);
+        g_wavetimes[5 * gb + 0] = ((unsigned long long)xcc << 32) | hw;
+        g_wavetimes[5 * gb + 1] = t0;
+        g_wavetimes[5 * gb + 2] = t1;
+        g_wavetimes[5 * gb + 3] = r0;
+        g_wavetimes[5 * gb + 4] = r1;
+    }
+#endif
+}
+#endif
 
 }  // namespace smi

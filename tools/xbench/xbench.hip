@@ -168,6 +168,11 @@ int main(int argc, char **argv) {
                  "\"vgprs\": %d, \"lds\": %zu, \"per_cu\": %d, \"nb\": %d, \"nb_ce\": %d, \"wcone\": %d, \"tasks\": %d, "
                  "\"resident\": %d",
                  fa.numRegs, fa.sharedSizeBytes, per_cu, g.nb, g.nb_ce, g.wcone, g.tasks, waves);
+#ifdef SMI_X_WAVETIMES
+        unsigned long long *wt = nullptr;
+        CK(hipMalloc(&wt, (size_t)3 * 8 * g.tasks));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(smi::g_wavetimes), &wt, sizeof(wt)));
+#endif
         timeit("sweepx", K, n, launches, warm,
                [&](bool flip) {
                    smi::SweepKArgs la = args;
@@ -178,12 +183,32 @@ int main(int argc, char **argv) {
                    hipLaunchKernelGGL((smi::sweepx_kernel<K>), dim3(blocks), dim3(256), 0, 0, la, g);
                },
                b, r0, extra);
+#ifdef SMI_X_WAVETIMES
+        {
+            // the last launch's waves: per SIMD (xcc, se, sh, cu, simd), the
+            // older / younger wave's start and end relative to the launch start
+            std::vector<unsigned long long> h(3 * (size_t)g.tasks);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(h.data(), wt, h.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull, t1 = 0;
+            for (int i = 0; i < g.tasks; ++i) t0 = std::min(t0, h[3 * i + 1]), t1 = std::max(t1, h[3 * i + 2]);
+            FILE *f = fopen("wavetimes.csv", "w");
+            fprintf(f, "wave,xcc,hw_id,wave_slot,simd,cu,sh,se,start,end\n");
+            for (int i = 0; i < g.tasks; ++i) {
+                const unsigned hw = (unsigned)h[3 * i], xcc = (unsigned)(h[3 * i] >> 32);
+                fprintf(f, "%d,%u,%u,%u,%u,%u,%u,%u,%llu,%llu\n", i, xcc, hw, hw & 15, (hw >> 4) & 3, (hw >> 8) & 15,
+                        (hw >> 12) & 1, (hw >> 13) & 7, h[3 * i + 1] - t0, h[3 * i + 2] - t0);
+            }
+            fclose(f);
+            printf("{\"wavetimes\": \"wavetimes.csv\", \"launch_cycles\": %llu}\n", t1 - t0);
+        }
+#endif
         CK(hipMemset(b, 0, cells * 4));
         CK(hipMemcpy(a, h.data(), cells * 4, hipMemcpyHostToDevice));
     }
 #endif
 #ifndef XB_NO_D
-    if (which == "d" || which == "both") {
+    if (which.find('d') != std::string::npos || which == "both") {
         int per_cu = 0;
         CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, smi::sweepd_kernel<K>, 256, 0));
         hipFuncAttributes fa;
@@ -213,6 +238,75 @@ int main(int argc, char **argv) {
                    hipLaunchKernelGGL((smi::sweepd_kernel<K>), dim3(blocks), dim3(256), 0, 0, la, g);
                },
                b, r0, extra);
+    }
+#endif
+#ifdef SMI_X_UNEQUAL
+    if (which.find('u') != std::string::npos) {
+        // the d geometry with nrb, nrb_ce even; pair tasks split fo/256 : rest
+        int per_cu = 0;
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, smi::sweepu_kernel<K>, 256, 0));
+        hipFuncAttributes fa;
+        CK(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(smi::sweepu_kernel<K>)));
+        const int waves = per_cu * cus * 4;
+        const int ce16 = 16 + 10, rev16 = 6;
+        const int fo = env("XB_FO", 167);
+        smi::SweepDGeom g{};
+        g.nstrips = st.nstrips;
+        g.n_int = st.n_int;
+        g.int0 = st.int0;
+        for (int k = 0; k < 4; ++k) g.ce[k] = st.ce[k];
+        g.wlast = std::max(4, std::min(16, 256 / (16 + rev16)));
+        g.nrb = (int)((long)waves * 16 / ((long)st.n_int * 16 + (long)st.nce * ce16)) & ~1;
+        g.nrb_ce = std::max(g.nrb, g.nrb * ce16 / 16) & ~1;
+        g.tasks = g.n_int * g.nrb + st.nce * g.nrb_ce;
+        const int P = (((g.tasks / 2 + 3) / 4) + 7) & ~7;  // b and b + P on one XCD
+        // every half at least K + 1 rows (the shortest: the young half of a pair)
+        const int bmin = n / g.nrb_ce;
+        if (bmin * (256 - std::max(fo, 256 - fo)) / 256 < K + 1) {
+            fprintf(stderr, "sweepu: halves too short\n");
+            return 1;
+        }
+        snprintf(extra, sizeof extra,
+                 "\"vgprs\": %d, \"per_cu\": %d, \"nrb\": %d, \"nrb_ce\": %d, \"tasks\": %d, \"resident\": %d, "
+                 "\"P\": %d, \"fo\": %d",
+                 fa.numRegs, per_cu, g.nrb, g.nrb_ce, g.tasks, waves, P, fo);
+#ifdef SMI_X_WAVETIMES
+        unsigned long long *wt = nullptr;
+        CK(hipMalloc(&wt, (size_t)5 * 8 * g.tasks));
+        CK(hipMemset(wt, 0, (size_t)5 * 8 * g.tasks));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(smi::g_wavetimes), &wt, sizeof(wt)));
+#endif
+        timeit("sweepu", K, n, launches, warm,
+               [&](bool flip) {
+                   smi::SweepKArgs la = args;
+                   if (flip) {
+                       la.in = args.out;
+                       la.out = const_cast<float *>(args.in);
+                   }
+                   hipLaunchKernelGGL((smi::sweepu_kernel<K>), dim3(2 * P), dim3(256), 0, 0, la, g, P, fo);
+               },
+               b, r0, extra);
+#ifdef SMI_X_WAVETIMES
+        {
+            std::vector<unsigned long long> h(5 * (size_t)g.tasks);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(h.data(), wt, h.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull;
+            unsigned long long rt0 = ~0ull;
+            for (int i = 0; i < g.tasks; ++i)
+                if (h[5 * i + 4]) t0 = std::min(t0, h[5 * i + 1]), rt0 = std::min(rt0, h[5 * i + 3]);
+            FILE *f = fopen("wavetimes_u.csv", "w");
+            fprintf(f, "wave,xcc,hw_id,wave_slot,simd,cu,sh,se,start,end,rstart,rend\n");
+            for (int i = 0; i < g.tasks; ++i) {
+                if (!h[5 * i + 4]) continue;
+                const unsigned hw = (unsigned)h[5 * i], xcc = (unsigned)(h[5 * i] >> 32);
+                fprintf(f, "%d,%u,%u,%u,%u,%u,%u,%u,%llu,%llu,%llu,%llu\n", i, xcc, hw, hw & 15, (hw >> 4) & 3,
+                        (hw >> 8) & 15, (hw >> 12) & 1, (hw >> 13) & 7, h[5 * i + 1] - t0, h[5 * i + 2] - t0,
+                        h[5 * i + 3] - rt0, h[5 * i + 4] - rt0);
+            }
+            fclose(f);
+        }
+#endif
     }
 #endif
     return 0;
