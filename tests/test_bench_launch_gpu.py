@@ -30,6 +30,9 @@ def test_bench_self_launch_two_ranks(gpu):
     assert d["config"]["decomposition"] == [1, 2] and d["config"]["fake_host"]
     assert d["config"]["launch"].startswith("self")
     assert d["roofline"]["kernels"], d["roofline"]
+    # repetition statistics of the timed plan (max over ranks per run)
+    r = d["repeats"]
+    assert r["runs"] >= 5 and 0 < r["min"] <= r["median"] <= r["max"] and r["stddev"] >= 0, r
     # the timed plan re-run from the seeded inputs and checked per rank on its
     # light cone against the oracle, verdict agreed by both ranks
     p = d["parity"]

@@ -250,6 +250,28 @@ struct SweepX {
         if constexpr (TC < 0 || TC == 2 * K) store_row<REV, SC>(t, v);
         return;
 #endif
+#ifdef SMI_X_LANEMASK
+        // experiment: level l needs lanes [m, 64 - m), m = (l - 1) / 4 (the
+        // cone's valid columns plus the lanes their DPP reads come from);
+        // the rest run with EXEC off (a lane-op and its register reads saved)
+        if constexpr (TC < 0) {
+            static_assert(K % 4 == 0, "lane-mask groups of 4 levels");
+            static_for<K / 4>([&](auto M) {
+                constexpr int m = M;
+                if (m == 0 || (lane >= m && lane < 64 - m)) {
+                    static_for<4>([&](auto L4) {
+                        constexpr int l = 4 * m + L4 + 1;
+                        constexpr int ia = ph(D + 2 * l, J), ib = ph(D + 2 * l - 1, J);
+                        float4 nv = step<REV, CE, SC>(R[ia], R[ib], v);
+                        if constexpr (l < K) R[ia] = nv;
+                        v = nv;
+                    });
+                }
+            });
+            store_row<REV, SC>(t, v);
+            return;
+        }
+#endif
         static_for<K>([&](auto L) {
             constexpr int l = L + 1;
             if constexpr (TC < 0 || TC >= 2 * l) {
