@@ -781,7 +781,12 @@ def main() -> None:
     g = seeded_tile(rank, X, Y)
     tile = torch.from_numpy(g).cuda()
     scratch = torch.empty_like(tile)
-    stream = torch.cuda.Stream()
+    # the highest priority, like the communicator's comm stream: a stream at
+    # normal priority can share a hardware queue with RCCL's own streams, and
+    # the library then runs the interior on a stream of its own, joined to
+    # this one at the start and end of each run (stencil_run.cpp
+    # interior_stream); at the highest priority the interior runs right here
+    stream = torch.cuda.Stream(priority=-1)
 
     fusion = stencil.get_fusion()
     K = fusion["steps_per_pass"]

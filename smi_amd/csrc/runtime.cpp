@@ -282,6 +282,7 @@ int smi_finalize(SMI_Comm comm) {
     }
     SMI_HIP_CHECK(hipSetDevice(c->device));
     if (c->comm_stream) SMI_HIP_CHECK(hipStreamSynchronize(c->comm_stream));
+    if (c->interior_stream) SMI_HIP_CHECK(hipStreamSynchronize(c->interior_stream));
     SMI_HIP_CHECK(hipDeviceSynchronize());
     int drain_rc = channels_drain(c.get());
     c->chan_engine.reset();
@@ -290,6 +291,7 @@ int smi_finalize(SMI_Comm comm) {
     if (c->work) SMI_HIP_CHECK(hipFree(c->work));
     if (c->halo) SMI_HIP_CHECK(hipFree(c->halo));
     if (c->comm_stream) SMI_HIP_CHECK(hipStreamDestroy(c->comm_stream));
+    if (c->interior_stream) SMI_HIP_CHECK(hipStreamDestroy(c->interior_stream));
     return drain_rc;
 }
 

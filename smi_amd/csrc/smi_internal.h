@@ -116,6 +116,9 @@ struct Comm {
     int device = 0;
     std::unique_ptr<Transport> transport;
     hipStream_t comm_stream = nullptr;  // dedicated halo / collective stream
+    // the multi-rank stencil's interior stream when the caller's stream is not
+    // at the highest priority (stencil_run.cpp interior_stream), made on demand
+    hipStream_t interior_stream = nullptr;
     // device workspace (grown on demand, never shrunk)
     void *work = nullptr;
     size_t work_bytes = 0;

@@ -16,6 +16,69 @@ struct Neighbours {
     int tl = -1, tr = -1, bl = -1, br = -1;             // diagonals (depth-2 corners only)
 };
 
+// The pass-boundary join of the K-step passes.  interior(t) reads the bands
+// band(t-1) wrote on the comm stream.  A stream wait on its event costs a
+// barrier packet on the main stream -- ~7-10 us between two interiors even
+// when band(t-1) finished long before (tools/streambench).
+// band(t-1) runs beside interior(t-1) and normally ends well inside it, so the
+// host watches it instead: once hipEventQuery reports it complete (its
+// end-of-kernel release done), interior(t) is enqueued behind interior(t-1)
+// with no wait packet, and its own dispatch acquire makes the bands visible.
+// Should interior(t-1) finish first, the host still waits for band(t-1): a
+// wait packet on the library's own interior stream measured far worse than
+// the host's few microseconds (0.70 vs 0.91 of a lone tile).
+// The host only waits for work already enqueued, so no rank's host can block
+// another's (every exchange up to t-1 was posted before).
+static bool host_join_enabled() {
+#ifdef SMI_LOOPBACK_REHEARSAL
+    if (const char *v = getenv("SMI_HOST_JOIN")) return atoi(v) != 0;  // rehearsal A/B
+#endif
+    return true;
+}
+
+static int join_band(hipEvent_t band_prev) {
+    for (;;) {
+        const hipError_t q = hipEventQuery(band_prev);
+        if (q == hipSuccess) return SMI_SUCCESS;
+        if (q != hipErrorNotReady) SMI_HIP_CHECK(q);
+    }
+}
+
+// The stream the multi-rank interior runs on.  HIP maps streams onto
+// GPU_MAX_HW_QUEUES (default 4) hardware queues per priority and shares a
+// queue between streams beyond that; RCCL makes streams of its own.  A
+// caller's stream at normal priority created after the communicator landed
+// on a queue RCCL's work also uses, and the interior then serialised with the
+// exchange: 0.70-0.79 of a lone tile instead of 0.92-0.94 in the interior-rank
+// rehearsal (profiles/r05/rehearsal/queues/).  The comm stream is at the
+// highest priority; an interior stream there as well gets a queue of its own.
+// So a caller's stream at the highest priority is used as it is; any other
+// is joined to an interior stream of the communicator at that priority (a
+// wait only when the caller's stream still has work pending) and joins it
+// back at the end of the run.
+static int interior_stream(Comm *c, hipStream_t user, hipStream_t *out, bool *own) {
+    int least = 0, greatest = 0, prio = 0;
+    SMI_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    SMI_HIP_CHECK(hipStreamGetPriority(user, &prio));
+    *out = user;
+    *own = false;
+    if (prio == greatest) return SMI_SUCCESS;
+    if (!c->interior_stream)
+        SMI_HIP_CHECK(hipStreamCreateWithPriority(&c->interior_stream, hipStreamNonBlocking, greatest));
+    const hipError_t q = hipStreamQuery(user);
+    if (q == hipErrorNotReady) {
+        hipEvent_t ev;
+        SMI_TRY(comm_event(c, 3, &ev));
+        SMI_HIP_CHECK(hipEventRecord(ev, user));
+        SMI_HIP_CHECK(hipStreamWaitEvent(c->interior_stream, ev, 0));
+    } else if (q != hipSuccess) {
+        SMI_HIP_CHECK(q);
+    }
+    *out = c->interior_stream;
+    *own = true;
+    return SMI_SUCCESS;
+}
+
 // Depth-1 exchange: new first/last row -> rank above/below, packed first/last
 // column -> left/right rank; the four halo vectors come back from them.
 static int exchange1(Comm *c, const Neighbours &nb, const float *tile, int rows, int cols, float *h_top,
@@ -495,9 +558,15 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
         return SMI_SUCCESS;
     }
 
-    hipEvent_t ev_edge, ev_int;
+    hipEvent_t ev_edge, ev_int, ev_edge_alt, ev_fin;
     SMI_TRY(comm_event(c, 0, &ev_edge));
     SMI_TRY(comm_event(c, 1, &ev_int));
+    SMI_TRY(comm_event(c, 2, &ev_edge_alt));
+    SMI_TRY(comm_event(c, 4, &ev_fin));
+    const bool overlap = g_tune.overlap != 0;
+    const hipStream_t user = s;
+    bool own_stream = false;
+    if (overlap) SMI_TRY(interior_stream(c, user, &s, &own_stream));
 
     // Halo staging.  Depth 2 (its inner row/column doubles as the depth-1
     // halo): top2 | bot2 | left2 | right2 | corner(4) | send_left2 |
@@ -551,6 +620,9 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     };
     auto xchg2 = [&](const float *tile, hipStream_t st) { return exchange2(c, nb, tile, rows, cols, hb, st); };
 
+    int kpass = 0;                 // K-step passes of the current phase
+    hipEvent_t last_band = nullptr;  // completion of the phase's last band kernel (host join)
+
     // Schedule (two streams, no host synchronisation between passes):
     //   comm stream : [wait interior(t-1)] band(t) -> rec E_edge(t) -> exchange(t)
     //   main stream : [wait E_edge(t-1)] interior(t)    -> rec E_int(t)
@@ -563,7 +635,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     // from halos of the current state: the neighbours' current edges (for
     // the first phase the reference's artificial timestep t=0,
     // stencil_smi.cl:26-29,183-224).
-    const bool overlap = g_tune.overlap != 0;
+    const bool host_join = overlap && host_join_enabled();
     auto phase_start = [&]() -> int {
         SMI_HIP_CHECK(hipEventRecord(ev_int, s));
         SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
@@ -575,7 +647,19 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
     // between kernels; ~4 us per pass, tools/streambench); the other phases'
     // kernels ignore it and it is recorded after them here.
     auto pass = [&](auto ring, auto interior, auto xchg, bool need_xchg, const float *out, bool carries) -> int {
-        if (overlap) {
+        if (overlap && carries && host_join) {
+            // K-step passes, host-observed join (see join_band above):
+            // band(t) carries ev_band[t & 1]; interior(t) follows band(t-1)
+            // with no wait packet when the host has seen band(t-1) finish
+            hipEvent_t ev_cur = (kpass & 1) ? ev_edge_alt : ev_edge, ev_prev = (kpass & 1) ? ev_edge : ev_edge_alt;
+            SMI_TRY(ring(cs, ev_cur));
+            if (kpass > 0) SMI_TRY(join_band(ev_prev));
+            SMI_TRY(interior(s, ev_int));
+            if (need_xchg) SMI_TRY(xchg(out, cs));
+            SMI_HIP_CHECK(hipStreamWaitEvent(cs, ev_int, 0));
+            last_band = ev_cur;
+            ++kpass;
+        } else if (overlap) {
             // The interior is enqueued before the exchange: posting the
             // transport's sends/receives costs host time (RCCL group, or
             // event + copy per message in-process) that must not delay the
@@ -615,6 +699,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             };
             SMI_TRY(launch_packk(bufp(cur), rows, cols, K, hkv, cs));
             SMI_TRY(xchgk(bufp(cur), cs));
+            kpass = 0;
             for (int p = 0; p < npass; ++p, cur ^= 1) {
                 bk.in = ak.in = bufp(cur);
                 bk.out = ak.out = bufp(cur ^ 1);
@@ -626,6 +711,8 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
                              },
                              xchgk, p < npass - 1, ak.out, true));
             }
+            // whatever runs next on the main stream reads the last bands
+            if (host_join && last_band) SMI_HIP_CHECK(hipStreamWaitEvent(s, last_band, 0));
         } else if (K == 2) {
             // ---- pairs of steps (depth-2 halos)
             SMI_TRY(launch_pack2(bufp(cur), rows, cols, h2, cs));
@@ -661,9 +748,14 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             }
         }
     }
-    // the caller's stream owns the result: join the comm stream
+    // the caller's stream owns the result: join the comm stream (and the
+    // interior stream when the run had one)
     SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
-    SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));
+    SMI_HIP_CHECK(hipStreamWaitEvent(user, ev_edge, 0));
+    if (own_stream) {
+        SMI_HIP_CHECK(hipEventRecord(ev_fin, s));
+        SMI_HIP_CHECK(hipStreamWaitEvent(user, ev_fin, 0));
+    }
     return SMI_SUCCESS;
 }
 

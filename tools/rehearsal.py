@@ -17,7 +17,10 @@ free for the band kernel and the exchange (smi_stencil_set_bands),
 REHEARSAL_LEAN (list, default 1) the band kernel for K >= 13 (1 = the lean
 kernel beside the interior, 0 = one wave per segment).
 REHEARSAL_PROF=0 times the runs without the library's profiling markers (the
-band / interior averages are then not reported).
+band / interior averages are then not reported).  Python's garbage collector
+is off inside each timed run (REHEARSAL_GC=1 leaves it on).  efficiency = min
+over the lone-tile runs / min over the interior-rank runs, efficiency_median
+the same with medians.
 SMI_LOOPBACK_FUSED=1 prices the exchange as one copy kernel (like one RCCL
 group), SMI_LOOPBACK_NOXCHG=1 leaves it out, SMI_LOOPBACK_HEAVY=<blocks> as
 one copy kernel of that many 256-thread workgroups with rcclGenericKernel's
@@ -27,6 +30,7 @@ one-rank RCCL communicator whose 8 sends and receives go to itself (RCCL's
 self send/recv, one group per pass, the production RcclTransport).
 usage: rehearsal.py [tile] [K...]
 """
+import gc
 import json
 import os
 import sys
@@ -53,17 +57,43 @@ def timed(comm, t, sc, steps, reps=5):
     return sorted(runs)
 
 
+_STREAM = []
+
+
+def _new_stream():
+    # REH_STREAM_PRIO=high: the run's stream at the highest priority (the
+    # library then runs the interior on it); by default at normal priority,
+    # created after the communicator, as a caller would (the library then
+    # moves the interior to a stream of its own at the highest priority)
+    return torch.cuda.Stream(priority=-1 if os.environ.get("REH_STREAM_PRIO") == "high" else 0)
+
+
 def _timed(comm, t, sc, steps):
-    s = torch.cuda.Stream()
+    # one stream for every run: a new torch stream per run (rounds 3-5) made
+    # every few runs land on the comm stream's hardware queue (HIP maps
+    # streams round-robin onto GPU_MAX_HW_QUEUES = 4 queues), serialising the
+    # interior with the bands and the exchange -- the series' "slow run"
+    if not _STREAM:
+        _STREAM.append(_new_stream())
+    s = _STREAM[0]
     with torch.cuda.stream(s):
         stencil.run(comm, t, 2 * steps, 1, 1, sc)
         s.synchronize()
         profiling.reset()
         profiling.enable(os.environ.get("REHEARSAL_PROF", "1") != "0")
-        t0 = time.perf_counter()
-        stencil.run(comm, t, steps, 1, 1, sc)
-        s.synchronize()
-        dt = time.perf_counter() - t0
+        # no garbage-collector pass inside a timed run (a C/C++ host has
+        # none; round 5 traced the "slow run" of every series to one)
+        gc_on = os.environ.get("REHEARSAL_GC", "0") != "0"
+        gc.collect()
+        if not gc_on:
+            gc.disable()
+        try:
+            t0 = time.perf_counter()
+            stencil.run(comm, t, steps, 1, 1, sc)
+            s.synchronize()
+            dt = time.perf_counter() - t0
+        finally:
+            gc.enable()
         profiling.enable(False)
     return dt / steps * 1e3
 
@@ -84,6 +114,8 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
     ks = [int(k) for k in sys.argv[2:]] or [12]
     smi_amd.load(build_if_missing=False)
+    if os.environ.get("REH_STREAM_EARLY"):  # the run's stream created before the communicator
+        _STREAM.append(_new_stream())
     if os.environ.get("REHEARSAL_TRANSPORT") == "rccl":
         comm = smi_amd.Comm.create(0, 1, 0, smi_amd.Comm.unique_id())
     else:
@@ -108,8 +140,8 @@ def main():
                 # the lone tile right before each setting (the GPU clock
                 # drifts between settings and boxes)
                 os.environ.pop("SMI_LOOPBACK", None)
-                alone = min(alone, timed(comm, t, sc, steps)[0]) if os.environ.get("REHEARSAL_ALONE_MIN") else \
-                    timed(comm, t, sc, steps)[0]
+                alone_runs = timed(comm, t, sc, steps)
+                alone = min(alone, alone_runs[0]) if os.environ.get("REHEARSAL_ALONE_MIN") else alone_runs[0]
                 os.environ["SMI_LOOPBACK"] = "1"
                 runs = timed(comm, t, sc, steps)
                 loop = runs[0]
@@ -122,7 +154,11 @@ def main():
                                   "efficiency": round(alone / loop, 4),
                                   "runs_ms_per_step": [round(r, 5) for r in runs],
                                   "runs_chronological": [round(r, 5) for r in LAST_CHRONO],
-                                  "efficiency_median": round(alone / runs[len(runs) // 2], 4),
+                                  "alone_runs_ms_per_step": [round(r, 5) for r in alone_runs],
+                                  # median of the lone-tile runs / median of the interior-rank runs
+                                  "efficiency_median": round(alone_runs[len(alone_runs) // 2] / runs[len(runs) // 2], 4),
+                                  "gc_in_timed_runs": os.environ.get("REHEARSAL_GC", "0") != "0",
+                                  "run_stream_priority": "high" if os.environ.get("REH_STREAM_PRIO") == "high" else "normal",
                                   "band_avg_ms": round(band[0] / max(band[1], 1), 5),
                                   "interior_avg_ms": round(sweep[0] / max(sweep[1], 1), 5)}), flush=True)
     stencil.set_tuning(overlap=1)

@@ -47,6 +47,37 @@ __global__ void copy_wait_kernel(const float4 *__restrict__ in, float4 *__restri
         out[i] = in[i];
 }
 
+// mode 16 / 17: the flag is written by a one-thread kernel after the band
+// stand-in on the comm stream (the band's own end-of-kernel release makes its
+// stores visible); the big kernel's checking blocks (16: the first 64, 17: all)
+// read it with a relaxed device-coherent load and pay the acquire (L2
+// invalidate) only when they had to wait
+__global__ void set_flag_kernel(unsigned *flag, unsigned value) {
+    __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void copy_check_kernel(const float4 *__restrict__ in, float4 *__restrict__ out, size_t n,
+                                  const unsigned *flag, unsigned target, unsigned checkers) {
+    if (blockIdx.x < checkers) {
+        if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
+            target) {
+            while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
+                   target)
+                __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+    }
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
+// mode 18: a one-wave gate kernel before the big one on the main stream
+// spins on the flag (relaxed, device-coherent); the big kernel is unchanged
+__global__ void gate_kernel(const unsigned *flag, unsigned target) {
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
+           target)
+        __builtin_amdgcn_s_sleep(2);
+}
+
 __global__ void small_flag_kernel(float *out, int iters, unsigned *count, unsigned *flag, unsigned value) {
     float v = threadIdx.x;
     for (int i = 0; i < iters; ++i) v = v * 1.0000001f + 0.5f;
@@ -107,7 +138,7 @@ static void small_ev(Ctx &c, hipStream_t st, hipEvent_t stop) {
 // big kernel is armed while its predecessor still runs (round 5)
 static double run(Ctx &c, int mode, int passes) {
     CK(hipDeviceSynchronize());
-    if (mode == 13) {
+    if (mode == 13 || mode >= 16) {
         CK(hipMemset(c.dflag, 0, 4));
         CK(hipMemset(c.dcount, 0, 4));
         CK(hipDeviceSynchronize());
@@ -176,6 +207,22 @@ static double run(Ctx &c, int mode, int passes) {
                                (unsigned)(p + 1));
             hipExtLaunchKernelGGL(copy_wait_kernel, dim3(4096), dim3(256), 0, c.s, nullptr, c.e_int, 0,
                                   p & 1 ? c.b : c.a, p & 1 ? c.a : c.b, c.n, (const unsigned *)c.dflag, (unsigned)p);
+        } else if (mode == 16 || mode == 17) {
+            // cs: [wait big(t-1)] band(t), set flag = t + 1;
+            // s: big(t) back to back, no wait packet; its checking blocks
+            // wait for flag >= t (band(t-1) done)
+            if (p > 0) CK(hipStreamWaitEvent(c.cs, c.e_int, 0));
+            small(c, c.cs);
+            hipLaunchKernelGGL(set_flag_kernel, dim3(1), dim3(1), 0, c.cs, c.dflag, (unsigned)(p + 1));
+            hipExtLaunchKernelGGL(copy_check_kernel, dim3(4096), dim3(256), 0, c.s, nullptr, c.e_int, 0,
+                                  p & 1 ? c.b : c.a, p & 1 ? c.a : c.b, c.n, (const unsigned *)c.dflag, (unsigned)p,
+                                  mode == 16 ? 64u : 4096u);
+        } else if (mode == 18) {
+            if (p > 0) CK(hipStreamWaitEvent(c.cs, c.e_int, 0));
+            small(c, c.cs);
+            hipLaunchKernelGGL(set_flag_kernel, dim3(1), dim3(1), 0, c.cs, c.dflag, (unsigned)(p + 1));
+            hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, c.s, (const unsigned *)c.dflag, (unsigned)p);
+            big_ev(c, p, c.e_int);
         } else if (mode == 14 || mode == 15) {
             // streams swap roles every pass: big(p) on A = (p even ? s : cs),
             // small(p) on B after big(p-1) by queue order (big(p-1) ran on B),
@@ -231,7 +278,7 @@ int main(int argc, char **argv) {
             CK(hipStreamCreateWithPriority(&c.cs, hipStreamNonBlocking, prio ? greatest : least));
             CK(hipEventCreateWithFlags(&c.e_int, evflags[ef]));
             CK(hipEventCreateWithFlags(&c.e_band, evflags[ef]));
-            for (int mode = 0; mode < 16; mode += (mode == 2 ? 6 : 1)) {
+            for (int mode = 0; mode < 19; mode += (mode == 2 ? 6 : 1)) {
                 run(c, mode, 20);  // warm-up
                 const double us = run(c, mode, passes);
                 printf("{\"mode\": %d, \"comm_prio\": \"%s\", \"events\": \"%s\", \"us_per_pass\": %.2f}\n", mode,
