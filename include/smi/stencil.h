@@ -54,7 +54,14 @@ int smi_stencil_step(const float *in, float *out, int x_local, int y_local,
  * (0 or 1) names the buffer holding the final tile (like the reference's
  * half timesteps%2, stencil_smi.cpp:344; with fusion the index is
  * (K-step passes + pairs + remaining single steps) % 2).  Asynchronous w.r.t. the host
- * except for transport rendezvous. */
+ * except for transport rendezvous and, with neighbours, the K-step passes'
+ * pass-boundary join: before enqueueing interior(t) the host waits for the
+ * band kernel of pass t-1 (it ends inside interior(t-1)), so the call returns
+ * about one pass before the GPU finishes.  With neighbours the interior runs
+ * on `stream` if that is at the highest stream priority, else on a
+ * highest-priority stream of the communicator joined to `stream` at the start
+ * and end of the call (a normal-priority stream can share a hardware queue
+ * with RCCL's streams).  Results are identical either way. */
 int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local,
                     int y_local, int px, int py, int timesteps,
                     SMI_Stream stream, int *result_index);

@@ -141,15 +141,20 @@ def test_bad_arguments_raise(gpu):
         stencil.step(b, torch.empty_like(b), (1, 0, 0, 0))  # HALO side without halo
 
 
-def _decomposed_run(grid, T, PX, PY, overlap):
+def _decomposed_run(grid, T, PX, PY, overlap, priority=0, busy=False):
     from smi_amd import LocalGroup, stencil
     stencil.set_tuning(overlap=overlap)
     tiles = stencil.split_memory(grid, PX, PY)
 
     def rank_fn(comm):
-        s = torch.cuda.Stream()
+        s = torch.cuda.Stream(priority=priority)
         with torch.cuda.stream(s):
             t = torch.from_numpy(tiles[comm.rank]).cuda()
+            if busy:
+                # the tile is produced by work still queued on the caller's
+                # stream when the run is enqueued (t = t * 1 + 0 repeatedly)
+                for _ in range(20):
+                    t = torch.addcmul(torch.zeros_like(t), t, torch.ones_like(t))
             res = stencil.run(comm, t, T, PX, PY)
             s.synchronize()
             return res.cpu().numpy()
@@ -196,14 +201,14 @@ def test_full_size_8192_sweep(gpu, oracle_mod):
 
 
 # ------------------------------------------------ two steps per pass (fused) --
-def _run_fused(grid, T, PX=1, PY=1, overlap=1, ht2=0, u2=0, k=2):
+def _run_fused(grid, T, PX=1, PY=1, overlap=1, ht2=0, u2=0, k=2, priority=0, busy=False):
     from smi_amd import stencil
     old = stencil.get_fusion()
     stencil.set_fusion(k)
     oldk = stencil.get_fusion()
     stencil.set_fusion(k, ht2, u2)
     try:
-        return _decomposed_run(grid, T, PX, PY, overlap)
+        return _decomposed_run(grid, T, PX, PY, overlap, priority, busy)
     finally:
         stencil.set_fusion(k, oldk["rows_per_wave"] or -1, oldk["rows_in_flight"])
         stencil.set_fusion(old["steps_per_pass"], old["rows_per_wave"], old["rows_in_flight"])
@@ -465,6 +470,21 @@ def test_ring_decomposed(gpu, oracle_mod, k, pxpy, overlap):
     for T in (k, 2 * k + 3):
         got = _run_fused(g, T, PX, PY, overlap, k=k)
         assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, pxpy, T)
+
+
+@pytest.mark.parametrize("priority,busy", [(-1, False), (-1, True), (0, True)])
+@pytest.mark.parametrize("k", [13, 20])
+def test_ring_decomposed_caller_stream(gpu, oracle_mod, k, priority, busy):
+    """The caller's stream at the highest priority (the interior runs on it)
+    or at normal priority (the communicator's interior stream, joined to it),
+    with the tile still being produced on it when the run is enqueued: the
+    K-step passes' host-observed join and the stream joins are bit-neutral
+    (2x2 and 2x4 ranks, T = 2K + 3)."""
+    for PX, PY in ((2, 2), (2, 4)):
+        g = oracle_mod.init_uniform(136 * PX, 264 * PY, seed=PX * 7 + PY + k)
+        T = 2 * k + 3
+        got = _run_fused(g, T, PX, PY, 1, k=k, priority=priority, busy=busy)
+        assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (k, PX, PY, priority, busy)
 
 
 @pytest.mark.parametrize("k", [16, 20])
