@@ -711,8 +711,10 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
                              },
                              xchgk, p < npass - 1, ak.out, true));
             }
-            // whatever runs next on the main stream reads the last bands
-            if (host_join && last_band) SMI_HIP_CHECK(hipStreamWaitEvent(s, last_band, 0));
+            // whatever runs next on the main stream reads the last bands:
+            // joined on the host as well (no wait packet on the interior
+            // stream, see join_band)
+            if (host_join && last_band) SMI_TRY(join_band(last_band));
         } else if (K == 2) {
             // ---- pairs of steps (depth-2 halos)
             SMI_TRY(launch_pack2(bufp(cur), rows, cols, h2, cs));
