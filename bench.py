@@ -162,8 +162,7 @@ def cpu_baseline(budget_s: float = 2.0) -> dict:
       value       -- the stencil on every host thread this job may use
                      (OpenMP), 8192^2 tile stepped in place between two
                      preallocated buffers for ~budget_s (no allocation in
-                     the timed calls); legs.all_affinity_cpus: the same on
-                     every CPU of the affinity mask when that is more;
+                     the timed calls), on the job's CPU quota;
       legs.serial_reference_order -- the host Reference() loop order
                      (examples/host/stencil_smi.cpp:33-46) on 1 core;
       legs.emulator_config1 / emulator_2x4 -- the rank-decomposed program
@@ -202,15 +201,15 @@ def cpu_baseline(budget_s: float = 2.0) -> dict:
         "sample": f"{TILE}x{TILE} fp32 Jacobi, {steps} steps, OpenMP C restatement "
                   f"(oracle/smi_oracle.c oracle_stencil_steps: two preallocated buffers stepped in place) "
                   f"of stencil_smi.cl:117-165, {dt:.1f} s wall on {threads} threads "
-                  f"(this job's CPU share; all {cpu['affinity_cpus']} affinity CPUs in legs)",
+                  f"(this job's CPU quota, OMP_NUM_THREADS; the affinity mask spans {cpu['affinity_cpus']} CPUs "
+                  f"shared with other jobs)",
         **cpu,
     }
+    # no leg on every CPU of the affinity mask: the box's mask spans the whole
+    # machine (256 CPUs) while the job's CPU quota is OMP_NUM_THREADS (16), so
+    # such a leg measures oversubscription, not the CPU (round 5 read 0.47
+    # GCell/s on 256 threads against 48 on 16)
     legs = {}
-    if cpu["affinity_cpus"] != threads:
-        v_all, st_all, dt_all = rate(cpu["affinity_cpus"], min(1.0, budget_s))
-        legs["all_affinity_cpus"] = {"GCells": round(v_all, 3), "cores": cpu["affinity_cpus"],
-                                     "sample": f"{st_all} steps in {dt_all:.2f} s on every CPU of the "
-                                               f"affinity mask (beyond this job's share: contended)"}
     del bufs
     gs = g[:2048, :2048].copy()
     reps, dt = _time_loop(lambda: oracle.stencil(gs, 2, order="host", threads=1), 1.5)
@@ -856,6 +855,13 @@ def main() -> None:
         # ~2 s of them at most, 30 at most, 5 at least.
         rep_s = []
         n_rep = max(5, min(30, int(2.0 / max(t1 - t0, 1e-6))))
+        if world > 1:
+            # every rank must run the same count (each run carries halo
+            # exchanges that pair up across ranks): the ranks' own wall times
+            # can straddle an integer boundary, so agree on the largest
+            flag = torch.tensor([n_rep])
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            n_rep = int(flag.item())
         for _ in range(n_rep):
             barrier()
             torch.cuda.synchronize()

@@ -113,6 +113,20 @@ int smi_stencil_get_bands(int *reserve_waves, int *interior_rounds);
 int smi_stencil_set_band_kernel(int lean);
 int smi_stencil_get_band_kernel(int *lean);
 
+/* Multi-rank K-step passes (scheduling only, bit-neutral): how interior(t)
+ * is ordered after the band kernel of pass t-1.  1 (default) = on the host:
+ * smi_stencil_run waits for band(t-1) to finish (it ends inside
+ * interior(t-1)) and then enqueues interior(t) with no wait packet between
+ * two interiors (~5 us per pass less than a device-side wait); the host is
+ * then about one pass ahead of the GPU, so a host thread held up for longer
+ * than one pass (~150 us at 8192^2, K = 20) idles the GPU for the excess.
+ * 0 = on the device: a stream wait per pass; the host enqueues the whole
+ * run without waiting and absorbs host stalls of any length behind the
+ * queued passes, at ~3 % more GPU time per pass.
+ * host_join = -1 keeps the setting. */
+int smi_stencil_set_join(int host_join);
+int smi_stencil_get_join(int *host_join);
+
 /* The rotating-ring sweep (K = 13..20) launches one round of waves whose
  * row blocks are shortened where a wave has more work per row: ce16 / rev16
  * = the extra work of a wave holding a global-edge column / of the

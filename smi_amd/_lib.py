@@ -68,6 +68,8 @@ SIGNATURES = {
     "smi_stencil_get_bands": (I, [ctypes.POINTER(I)] * 2),
     "smi_stencil_set_band_kernel": (I, [I]),
     "smi_stencil_get_band_kernel": (I, [ctypes.POINTER(I)]),
+    "smi_stencil_set_join": (I, [I]),
+    "smi_stencil_get_join": (I, [ctypes.POINTER(I)]),
     "smi_stencil_set_deep": (I, [I, I, I]),
     "smi_stencil_deep_geometry": (I, [I, I, I, I] + [ctypes.POINTER(I)] * 5),
     "smi_stencil_get_deep": (I, [ctypes.POINTER(I)] * 3),

@@ -8,6 +8,7 @@ shipped in-tree to the GPU box.
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -202,18 +203,35 @@ def build_hosts(force: bool = False, verbose: bool = False) -> list[str]:
     os.makedirs(out_dir, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     outs = []
+    # a host is fresh when the content hash of its source, the hosts'
+    # shared headers, include/ and the library's own source hash matches the
+    # one recorded beside it (mtimes mislead on a copied tree)
+    common = sorted(glob.glob(os.path.join(HOSTS_DIR, "*.h")) + glob.glob(
+        os.path.join(ROOT, "include", "**", "*.h"), recursive=True))
+    with open(lib + ".srchash") as f:
+        lib_hash = f.read().strip()
     for src in sorted(glob.glob(os.path.join(HOSTS_DIR, "*.cpp"))):
         exe = os.path.join(out_dir, os.path.splitext(os.path.basename(src))[0])
         outs.append(exe)
-        if not force and os.path.exists(exe) and os.path.getmtime(exe) >= max(
-                os.path.getmtime(src), os.path.getmtime(lib)):
-            continue
         cmd = [hipcc, "-O2", "-std=c++17", "-Wall", f"-I{os.path.join(ROOT, 'include')}", src, "-o", exe,
                f"-L{OUT_DIR}", "-lsmi_amd", "-lpthread", "-Wl,-rpath,$ORIGIN/../../smi_amd/_build",
                f"-Wl,-rpath,{ROCM}/lib"]
+        h = hashlib.sha256(lib_hash.encode())
+        for p in [src] + common:
+            with open(p, "rb") as f:
+                h.update(os.path.relpath(p, ROOT).encode() + b"\0" + f.read())
+        h.update(" ".join(cmd).replace(ROOT, "<root>").encode())
+        digest = h.hexdigest()
+        stamp = exe + ".srchash"
+        if not force and os.path.exists(exe) and os.path.exists(stamp):
+            with open(stamp) as f:
+                if f.read().strip() == digest:
+                    continue
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
+        with open(stamp, "w") as f:
+            f.write(digest + "\n")
     return outs
 
 

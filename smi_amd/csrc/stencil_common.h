@@ -88,6 +88,7 @@ struct Tuning {
     // beside the interior sweep (bandl_kernel, <= 64 VGPRs, one workgroup per
     // CU), 0 = one wave per segment (bandk_kernel)
     int band_lean = 1;
+    int host_join = 1;  // smi_stencil_set_join
 };
 extern Tuning g_tune;
 

@@ -5,6 +5,9 @@
 // Convert{Send,Receive}{Top,Bottom,Left,Right} kernels of
 // examples/kernels/stencil_smi.cl:236-386, whose per-element SMI_Push/SMI_Pop
 // streams become one transport group of bulk sends/receives per exchange.
+#include <sched.h>
+
+#include <chrono>
 #include <cstdlib>
 
 #include "stencil_common.h"
@@ -33,14 +36,48 @@ static bool host_join_enabled() {
 #ifdef SMI_LOOPBACK_REHEARSAL
     if (const char *v = getenv("SMI_HOST_JOIN")) return atoi(v) != 0;  // rehearsal A/B
 #endif
-    return true;
+    return g_tune.host_join != 0;
 }
 
+#ifdef SMI_LOOPBACK_REHEARSAL
+// rehearsal: a host thread that falls behind -- SMI_REH_STALL_US of busy
+// host time before every SMI_REH_STALL_EVERY-th pass's interior is enqueued
+// (the same point under either join), to price what a descheduled host costs
+static void rehearsal_stall(int kpass) {
+    static const long us = getenv("SMI_REH_STALL_US") ? atol(getenv("SMI_REH_STALL_US")) : 0;
+    static const int every = getenv("SMI_REH_STALL_EVERY") ? std::max(1, atoi(getenv("SMI_REH_STALL_EVERY"))) : 10;
+    if (us <= 0 || kpass % every != every / 2) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(us)) {
+    }
+}
+#else
+static void rehearsal_stall(int) {}
+#endif
+
+// The wait: a short spin (the band normally ended long before, and a wake-up
+// after a sleep would cost the pass more than it saves), then the core is
+// yielded between polls, so that rank threads sharing the job's cores (the
+// in-process groups, the C++ hosts) reach their own transport rendezvous --
+// which band(t-1)'s exchange may be waiting for.  A band that never finishes
+// (a peer that failed, so exchange(t-2) never completes) is an error after
+// kJoinTimeout rather than a spin forever.
+static constexpr int kJoinSpinPolls = 64;
+static constexpr std::chrono::seconds kJoinTimeout{300};
+
 static int join_band(hipEvent_t band_prev) {
-    for (;;) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned polls = 0;; ++polls) {
         const hipError_t q = hipEventQuery(band_prev);
         if (q == hipSuccess) return SMI_SUCCESS;
         if (q != hipErrorNotReady) SMI_HIP_CHECK(q);
+        if (polls < kJoinSpinPolls) continue;
+        if ((polls & 1023) == 0 && std::chrono::steady_clock::now() - t0 > kJoinTimeout) {
+            set_error("smi_stencil_run: the band kernel of the previous pass did not finish within 300 s "
+                      "(a peer rank stopped exchanging halos?)");
+            return SMI_ERR_COMM;
+        }
+        sched_yield();
     }
 }
 
@@ -63,8 +100,16 @@ static int interior_stream(Comm *c, hipStream_t user, hipStream_t *out, bool *ow
     *out = user;
     *own = false;
     if (prio == greatest) return SMI_SUCCESS;
-    if (!c->interior_stream)
-        SMI_HIP_CHECK(hipStreamCreateWithPriority(&c->interior_stream, hipStreamNonBlocking, greatest));
+    if (!c->interior_stream) {
+        // made on the communicator's device whatever the calling thread's
+        // current device is (the stream lives as long as the communicator)
+        int cur = 0;
+        SMI_HIP_CHECK(hipGetDevice(&cur));
+        if (cur != c->device) SMI_HIP_CHECK(hipSetDevice(c->device));
+        const hipError_t e = hipStreamCreateWithPriority(&c->interior_stream, hipStreamNonBlocking, greatest);
+        if (cur != c->device) SMI_HIP_CHECK(hipSetDevice(cur));
+        SMI_HIP_CHECK(e);
+    }
     const hipError_t q = hipStreamQuery(user);
     if (q == hipErrorNotReady) {
         hipEvent_t ev;
@@ -383,6 +428,17 @@ int smi_stencil_get_band_kernel(int *lean) {
     return SMI_SUCCESS;
 }
 
+int smi_stencil_set_join(int host_join) {
+    SMI_ARG_CHECK(host_join <= 1, "pass join: 0 (device-side wait) or 1 (host-observed)");
+    if (host_join >= 0) g_tune.host_join = host_join;
+    return SMI_SUCCESS;
+}
+
+int smi_stencil_get_join(int *host_join) {
+    if (host_join) *host_join = g_tune.host_join;
+    return SMI_SUCCESS;
+}
+
 int smi_stencil_set_deep(int ce16, int rev16, int waves) {
     SMI_ARG_CHECK(ce16 <= 256 && rev16 <= 256 && waves <= (1 << 20), "deep sweep settings out of range");
     if (ce16 >= 0) g_tune.deep_ce16 = ce16;
@@ -653,6 +709,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             // with no wait packet when the host has seen band(t-1) finish
             hipEvent_t ev_cur = (kpass & 1) ? ev_edge_alt : ev_edge, ev_prev = (kpass & 1) ? ev_edge : ev_edge_alt;
             SMI_TRY(ring(cs, ev_cur));
+            rehearsal_stall(kpass);
             if (kpass > 0) SMI_TRY(join_band(ev_prev));
             SMI_TRY(interior(s, ev_int));
             if (need_xchg) SMI_TRY(xchg(out, cs));
@@ -667,6 +724,7 @@ int smi_stencil_run(SMI_Comm comm, float *buf0, float *buf1, int x_local, int y_
             // main stream idle ~100 us per pass behind the exchange calls.
             SMI_TRY(ring(cs, carries ? ev_edge : nullptr));
             if (!carries) SMI_HIP_CHECK(hipEventRecord(ev_edge, cs));
+            if (carries) rehearsal_stall(kpass++);
             SMI_TRY(interior(s, carries ? ev_int : nullptr));
             if (!carries) SMI_HIP_CHECK(hipEventRecord(ev_int, s));
             SMI_HIP_CHECK(hipStreamWaitEvent(s, ev_edge, 0));

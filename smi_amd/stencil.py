@@ -155,6 +155,20 @@ def get_band_kernel() -> int:
     return v.value
 
 
+def set_join(host_join: int = -1) -> None:
+    """Multi-rank K-step pass join (bit-neutral): 1 = host-observed (default;
+    the host runs about one pass ahead of the GPU), 0 = a device-side stream
+    wait per pass (the host enqueues the whole run; ~3 % more GPU time per
+    pass, host stalls absorbed).  -1 keeps it (smi_stencil_set_join)."""
+    _lib.call("smi_stencil_set_join", host_join)
+
+
+def get_join() -> int:
+    v = ctypes.c_int()
+    _lib.call("smi_stencil_get_join", ctypes.byref(v))
+    return v.value
+
+
 def deep_geometry(rows: int, cols: int, k: int, side_mask: int = 0) -> dict:
     """The rotating-ring sweep's work split for one K-step pass (host only;
     with no device set the launch's waves first: set_deep(waves=...))."""

@@ -195,6 +195,25 @@ def test_band_kernel_setting_roundtrip_and_validate():
         stencil.set_band_kernel(old)
 
 
+def test_join_setting_roundtrip_and_validate():
+    """smi_stencil_set_join: 1 = host-observed pass join (default), 0 = a
+    device-side wait per pass; -1 keeps it, anything else is refused."""
+    from smi_amd import stencil
+    from smi_amd._lib import SMIError
+    old = stencil.get_join()
+    assert old == 1  # default (DESIGN.md §6)
+    try:
+        stencil.set_join(0)
+        assert stencil.get_join() == 0
+        stencil.set_join(-1)
+        assert stencil.get_join() == 0
+        with pytest.raises(SMIError):
+            stencil.set_join(2)
+        assert stencil.get_join() == 0
+    finally:
+        stencil.set_join(old)
+
+
 @pytest.mark.parametrize("waves", [1024, 2048, 3072])
 def test_deep_geometry_every_block_holds_k_rows(waves):
     """sweepd_geometry (smi_stencil_deep_geometry, host only) over every K =

@@ -9,6 +9,19 @@ programs restated without Python in the loop.
   rank + 1; the root checks n(n+1)/2), bulk smi_reduce and the per-element
   SMI_Reduce API.
 
+* hosts/broadcast_benchmark.cpp -- microbenchmarks/host/broadcast_benchmark.cpp:
+  20-166 with broadcast.cl (the root sends 0..n-1, every other rank checks
+  element i == i), bulk smi_bcast and the per-element SMI_Bcast API.
+* hosts/gesummv_smi_host.cpp -- examples/host/gesummv_smi.cpp:48-351: the
+  A = B = i, x = 1 pattern, smi_gesummv row-sharded, the rel. 1e-4 check.
+
+Every host runs its ranks either as threads of one process (in-process
+group) or as one process per rank (--rank/--size/--uid, smi_init over RCCL,
+hosts/host_rt.h) -- the one-process-per-GPU deployment of an 8-GPU node.
+On a one-GPU box every rank process gets its own NCCL_HOSTID (RCCL refuses
+two ranks on one device of one host), so the bytes move over RCCL's socket
+transport, as in tests/test_rccl_multiproc_gpu.py.
+
 The GPU tests run the binaries as child processes (never exec) and check the
 stencil result bit for bit against the committed golden hash of BASELINE
 config 1 and against the oracle.
@@ -16,7 +29,9 @@ config 1 and against the oracle.
 import hashlib
 import json
 import os
+import signal
 import subprocess
+import time
 
 import numpy as np
 import pytest
@@ -47,10 +62,83 @@ def test_hosts_build_and_fail_loudly_without_gpu():
     if torch.cuda.device_count() > 0:
         pytest.skip("a GPU is visible: the GPU tests run the hosts")
     for args in ([_exe("stencil_smi_host"), "256", "256", "2", "2", "32"],
-                 [_exe("reduce_benchmark"), "-n", "16", "-r", "0", "-i", "1", "-p", "2"]):
+                 [_exe("reduce_benchmark"), "-n", "16", "-r", "0", "-i", "1", "-p", "2"],
+                 [_exe("broadcast_benchmark"), "-n", "16", "-r", "0", "-i", "1", "-p", "2"],
+                 [_exe("gesummv_smi_host"), "-n", "64", "-m", "64", "-a", "1", "-c", "1", "-r", "1"]):
         r = _run(args)
         assert r.returncode == 2, r.stdout + r.stderr
         assert "no GPU visible" in r.stderr
+
+
+def test_hosts_process_mode_fails_loudly_without_gpu(tmp_path):
+    """The one-process-per-rank launch stops at its first C-ABI call too
+    (rank 0's smi_get_unique_id) with exit code 2, and leaves no id file."""
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is visible: the GPU tests run the hosts")
+    uid = tmp_path / "uid"
+    r = _run([_exe("stencil_smi_host"), "256", "256", "1", "2", "32", "--rank", "0", "--size", "2", "--uid", str(uid)])
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert "smi_get_unique_id" in r.stderr and not uid.exists()
+    r = _run([_exe("stencil_smi_host"), "256", "256", "1", "2", "32", "--rank", "2", "--size", "2", "--uid", str(uid)])
+    assert r.returncode == 1  # a malformed launch is a usage error
+
+
+def _launch_ranks(args, world, tmp_path, timeout=240, stall=None):
+    """One process per rank (--rank/--size/--uid), started with subprocess;
+    every rank is killed once one fails or the time limit passes.  Returns
+    (exit codes, outputs).  stall = (rank, every_s, for_s): that rank's
+    process is stopped (SIGSTOP) for for_s every every_s seconds while the
+    job runs -- a host descheduled at arbitrary points."""
+    import torch
+    ngpu = torch.cuda.device_count()  # does not initialise the GPU on this image
+    uid = tmp_path / f"uid_{world}_{time.monotonic_ns()}"
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        if ngpu < world:
+            env.update(NCCL_HOSTID=f"smi-host-test-{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+        procs.append(subprocess.Popen(args + ["--rank", str(r), "--size", str(world), "--uid", str(uid)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    t_end = time.monotonic() + timeout
+    lines0 = []
+    if stall:
+        # stop the victim only once the runs are under way (rank 0 has printed
+        # its first run time): a stop inside the HIP runtime's start-up makes
+        # it find no device
+        import threading
+        reader = threading.Thread(target=lambda: lines0.extend(iter(procs[0].stdout.readline, "")), daemon=True)
+        reader.start()
+        while not any(ln.startswith("run ") for ln in lines0) and procs[0].poll() is None:
+            if time.monotonic() > t_end:
+                break
+            time.sleep(0.002)
+    t_stall = time.monotonic() + (stall[1] if stall else 0)
+    while any(p.poll() is None for p in procs):
+        failed = any(p.poll() not in (None, 0) for p in procs)
+        if failed or time.monotonic() > t_end:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        if stall and time.monotonic() >= t_stall and procs[stall[0]].poll() is None:
+            victim = procs[stall[0]]
+            victim.send_signal(signal.SIGSTOP)
+            time.sleep(stall[2])
+            victim.send_signal(signal.SIGCONT)
+            t_stall = time.monotonic() + stall[1]
+        time.sleep(0.005 if stall else 0.05)
+    if stall:
+        reader.join(timeout=30)
+        outs = ["".join(lines0)] + [p.communicate()[0] for p in procs[1:]]
+        procs[0].wait()
+    else:
+        outs = [p.communicate()[0] for p in procs]
+    return [p.returncode for p in procs], outs
+
+
+def _log(rcs, outs):
+    return "\n".join(f"--- rank {r} (rc {rc})\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
 
 
 def _golden_config1():
@@ -103,3 +191,139 @@ def test_reduce_benchmark_host_kat(tmp_path, mode, n, ranks, runs):
     assert "Conf interval 99" in r.stdout
     lines = dat.read_text().splitlines()
     assert lines[0].startswith("#SMI Reduce") and len([ln for ln in lines if not ln.startswith("#")]) == runs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pxpy", [(2, 2), (1, 2)])
+def test_stencil_host_processes_config1_matches_golden(tmp_path, pxpy):
+    """BASELINE config 1 through the C++ host with one process per rank over
+    RCCL (smi_get_unique_id -> file -> smi_init; tiles scattered from and
+    gathered to rank 0): the reference check passes on rank 0 and the result
+    is bit-identical to the golden hash."""
+    out = tmp_path / "res.f32"
+    world = pxpy[0] * pxpy[1]
+    rcs, outs = _launch_ranks([_exe("stencil_smi_host"), "256", "256", str(pxpy[0]), str(pxpy[1]), "32",
+                               "--out", str(out)], world, tmp_path)
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    assert "Successfully verified result." in outs[0]
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == _golden_config1()
+
+
+@pytest.mark.gpu
+def test_stencil_host_processes_deep_passes_vs_oracle(tmp_path):
+    """A 2x2 grid of 512x512 tiles in four rank processes, 40 steps = two
+    K = 20 passes (rotating-ring interior, lean band kernel, the depth-20
+    exchange over RCCL, the host-observed pass join): bit-exact vs the
+    oracle, reference check passed."""
+    import oracle
+    out = tmp_path / "res.f32"
+    rcs, outs = _launch_ranks([_exe("stencil_smi_host"), "1024", "1024", "2", "2", "40", "--init", "uniform",
+                               "--repeat", "2", "--out", str(out)], 4, tmp_path)
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    got = np.fromfile(out, dtype=np.float32).reshape(1024, 1024)
+    # the host's uniform grid: std::mt19937(1234) + uniform_real_distribution
+    # is not numpy's, so regenerate it from the host itself at T = 0
+    out0 = tmp_path / "init.f32"
+    r = _run([_exe("stencil_smi_host"), "1024", "1024", "1", "1", "0", "--init", "uniform", "--out", str(out0)])
+    assert r.returncode == 0, r.stdout + r.stderr
+    g0 = np.fromfile(out0, dtype=np.float32).reshape(1024, 1024)
+    want = oracle.stencil(g0, 40)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_stencil_host_processes_with_a_stopped_rank(tmp_path):
+    """Rank 1's host is stopped (SIGSTOP) for 20 ms every 50 ms while two rank
+    processes run 30 repeats of 400 steps (20 K = 20 passes) on 4096x4096
+    tiles: the host-observed pass join (smi_stencil_run enqueues interior(t)
+    only after seeing band(t-1) finish) must not depend on the host keeping
+    up -- the result stays bit-exact vs the oracle.  The run times rank 0
+    prints show what the stalls cost the job."""
+    import oracle
+    out = tmp_path / "res.f32"
+    args = [_exe("stencil_smi_host"), "4096", "8192", "1", "2", "400", "--init", "uniform", "--repeat", "30",
+            "--out", str(out)]
+    rcs, outs = _launch_ranks(args, 2, tmp_path, stall=(1, 0.05, 0.02))
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    runs = [float(ln.split()[2]) for ln in outs[0].splitlines() if ln.startswith("run ")]
+    print("run times (s):", runs)
+    assert len(runs) == 30
+    print("stalled runs, median (s):", sorted(runs)[15])
+    got = np.fromfile(out, dtype=np.float32).reshape(4096, 8192)
+    out0 = tmp_path / "init.f32"
+    r = _run([_exe("stencil_smi_host"), "4096", "8192", "1", "1", "0", "--init", "uniform", "--out", str(out0)])
+    assert r.returncode == 0, r.stdout + r.stderr
+    want = oracle.stencil(np.fromfile(out0, dtype=np.float32).reshape(4096, 8192), 400)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,mode,n", [(2, "bulk", 1 << 20), (4, "bulk", 4096), (2, "element", 256)])
+def test_reduce_benchmark_processes_kat(tmp_path, world, mode, n):
+    """reduce.cl's known answer with one process per rank over RCCL."""
+    rcs, outs = _launch_ranks([_exe("reduce_benchmark"), "-n", str(n), "-r", "0", "-i", "3", "-m", mode],
+                              world, tmp_path)
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    assert outs[0].count("Result is Ok!") == 3 and "Conf interval 99" in outs[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,n,ranks,root", [("bulk", 1 << 20, 4, 0), ("bulk", 1000, 3, 2),
+                                               ("element", 512, 4, 1)])
+def test_broadcast_benchmark_host_kat(tmp_path, mode, n, ranks, root):
+    """broadcast.cl's check (element i arrives as i) on every non-root rank of
+    every run, threads as ranks, and the harness's statistics file."""
+    dat = tmp_path / "smi_broadcast.dat"
+    r = _run([_exe("broadcast_benchmark"), "-n", str(n), "-r", str(root), "-i", "3", "-p", str(ranks),
+              "-m", mode, "-o", str(dat)])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("Result is Ok!") == 3 * (ranks - 1) and "Error" not in r.stdout
+    assert "Average bandwidth (Gbit/s)" in r.stdout
+    lines = dat.read_text().splitlines()
+    assert lines[0].startswith("#SMI Broadcast") and len([ln for ln in lines if not ln.startswith("#")]) == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,mode,n", [(2, "bulk", 1 << 20), (4, "bulk", 100000), (2, "element", 256)])
+def test_broadcast_benchmark_processes_kat(tmp_path, world, mode, n):
+    """The same with one process per rank over RCCL."""
+    rcs, outs = _launch_ranks([_exe("broadcast_benchmark"), "-n", str(n), "-r", "0", "-i", "3", "-m", mode],
+                              world, tmp_path)
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    assert sum(o.count("Result is Ok!") for o in outs) == 3 * (world - 1)
+
+
+def _oracle_gesummv_pattern(n, m, alpha, beta):
+    import oracle
+    A = np.repeat(np.arange(n, dtype=np.float32)[:, None], m, axis=1)
+    return oracle.gesummv(A, A, np.ones(m, dtype=np.float32), alpha, beta)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,n,m", [(2, 1024, 2048), (8, 4096, 8192), (3, 1000, 4096)])
+def test_gesummv_host_reference_pattern(tmp_path, ranks, n, m):
+    """gesummv_smi's own test (A = B = i, x = 1, rel. 1e-4 vs sgemv) through
+    the C++ host, threads as ranks: "OK!!!", and y bit-identical to the
+    oracle's restatement of the row fold."""
+    y = tmp_path / "y.f32"
+    r = _run([_exe("gesummv_smi_host"), "-n", str(n), "-m", str(m), "-a", "1.5", "-c", "0.5", "-r", "3",
+              "-p", str(ranks), "-y", str(y)])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK!!!" in r.stdout
+    got = np.fromfile(y, dtype=np.float32)
+    assert np.array_equal(got.view(np.uint32), _oracle_gesummv_pattern(n, m, 1.5, 0.5).view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_gesummv_host_processes(tmp_path, world):
+    """The same with one process per rank over RCCL (y chunks streamed to
+    rank 0 over the transport)."""
+    y = tmp_path / "y.f32"
+    n, m = 2048, 4096
+    rcs, outs = _launch_ranks([_exe("gesummv_smi_host"), "-n", str(n), "-m", str(m), "-a", "2", "-c", "-0.25",
+                               "-r", "2", "-y", str(y)], world, tmp_path)
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    assert "OK!!!" in outs[0]
+    got = np.fromfile(y, dtype=np.float32)
+    assert np.array_equal(got.view(np.uint32), _oracle_gesummv_pattern(n, m, 2.0, -0.25).view(np.uint32))

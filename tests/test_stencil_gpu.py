@@ -528,6 +528,26 @@ def test_band_kernel_choice_is_bit_neutral(gpu, oracle_mod, k, pxpy):
         stencil.set_band_kernel(old)
 
 
+@pytest.mark.parametrize("k,pxpy,steps", [(20, (2, 2), 62), (13, (1, 3), 29), (12, (3, 1), 37)])
+def test_join_mode_is_bit_neutral(gpu, oracle_mod, k, pxpy, steps):
+    """smi_stencil_set_join: the host-observed pass join (1, default) and the
+    device-side stream wait per pass (0) give the same bits, both equal to
+    the oracle -- several K-step passes plus the remainder phases, so that
+    both joins are crossed many times."""
+    from smi_amd import stencil
+    PX, PY = pxpy
+    g = oracle_mod.init_uniform(200 * PX, 264 * PY, seed=k * 11 + PX)
+    want = bits(oracle_mod.stencil(g, steps))
+    old = stencil.get_join()
+    try:
+        for join in (1, 0):
+            stencil.set_join(join)
+            got = _run_fused(g, steps, PX, PY, 1, k=k)
+            assert np.array_equal(bits(got), want), (k, pxpy, join)
+    finally:
+        stencil.set_join(old)
+
+
 def test_ring_full_size_8192_driver_config(gpu, oracle_mod):
     """BASELINE config 2 at the driver's --steps 20 with K = 20: one pass of
     the rotating-ring sweep over 8192^2, bit-exact vs the oracle."""

@@ -39,19 +39,28 @@ def main():
             continue
         host = next((i for i in ints if i[0] <= s <= i[1]), None)
         rows.append((k, host is not None and e <= host[1], (e - host[1]) / 1e3 if host else None))
+    def med(v):
+        v = sorted(v)
+        return round(v[len(v) // 2] / 1e3, 1) if v else None
+
     summ = {}
     for k in ("band", "xchg"):
         r = [x for x in rows if x[0] == k]
         if r:
             summ[k] = {"launches": len(r), "inside_interior": sum(1 for x in r if x[1]),
-                       "max_overhang_us": round(max((x[2] for x in r if x[2] is not None), default=0.0), 1)}
+                       "max_overhang_us": round(max((x[2] for x in r if x[2] is not None), default=0.0), 1),
+                       "duration_median_us": med([e - s for s, e, kk in ev if kk == k and s >= t0])}
     if len(ints) > 1:
         last = ints[-n:]
         per = (last[-1][1] - last[0][0]) / len(last) / 1e3
+        durs = [e - s for s, e, _ in last]
+        gaps = [b[0] - a[1] for a, b in zip(last, last[1:])]
         print(f"interior pass period over the last {len(last)}: {per:.1f} us; "
-              f"interior duration avg {sum(e - s for s, e, _ in last) / len(last) / 1e3:.1f} us")
-        summ["interior"] = {"period_us": round(per, 1),
-                            "duration_avg_us": round(sum(e - s for s, e, _ in last) / len(last) / 1e3, 1)}
+              f"interior duration avg {sum(durs) / len(last) / 1e3:.1f} us")
+        summ["interior"] = {"period_us": round(per, 1), "passes": len(last),
+                            "duration_avg_us": round(sum(durs) / len(last) / 1e3, 1),
+                            "duration_median_us": med(durs), "duration_min_us": round(min(durs) / 1e3, 1),
+                            "duration_max_us": round(max(durs) / 1e3, 1), "gap_median_us": med(gaps)}
     print(json.dumps(summ))
 
 
