@@ -327,3 +327,55 @@ def test_gesummv_host_processes(tmp_path, world):
     assert "OK!!!" in outs[0]
     got = np.fromfile(y, dtype=np.float32)
     assert np.array_equal(got.view(np.uint32), _oracle_gesummv_pattern(n, m, 2.0, -0.25).view(np.uint32))
+
+
+# ------------------------------------------------ BASELINE configs 3-5 as rank processes --
+@pytest.mark.gpu
+def test_config3_stencil_16384_processes(tmp_path):
+    """BASELINE config 3 (16384^2 fp32 as 2x2 tiles of 8192^2, the halo
+    exchange over RCCL) with one process per rank: two K = 20 passes,
+    bit-exact vs the oracle and the reference check on rank 0."""
+    import oracle
+    out = tmp_path / "res.f32"
+    rcs, outs = _launch_ranks([_exe("stencil_smi_host"), "16384", "16384", "2", "2", "40", "--init", "uniform",
+                               "--out", str(out)], 4, tmp_path, timeout=400)
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    assert "Successfully verified result." in outs[0]
+    got = np.fromfile(out, dtype=np.float32).reshape(16384, 16384)
+    out0 = tmp_path / "init.f32"
+    r = _run([_exe("stencil_smi_host"), "16384", "16384", "1", "1", "0", "--init", "uniform", "--out", str(out0)])
+    assert r.returncode == 0, r.stdout + r.stderr
+    want = oracle.stencil(np.fromfile(out0, dtype=np.float32).reshape(16384, 16384), 40)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("host", ["reduce_benchmark", "broadcast_benchmark"])
+def test_config4_256mib_processes(tmp_path, host):
+    """BASELINE config 4 at its largest message (256 MiB of fp32) across four
+    rank processes: the reduce.cl / broadcast.cl known answers on every
+    element of every run."""
+    rcs, outs = _launch_ranks([_exe(host), "-n", str(64 << 20), "-r", "0", "-i", "2"], 4, tmp_path, timeout=400)
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    assert sum(o.count("Result is Ok!") for o in outs) == (2 if host == "reduce_benchmark" else 6)
+    assert not any("Error" in o for o in outs)
+
+
+@pytest.mark.gpu
+def test_config5_gesummv_32768_8_processes(tmp_path):
+    """BASELINE config 5 (gesummv 32768^2 fp32, rows sharded over 8 ranks,
+    y chunks streamed to the root) with one process per rank: the
+    reference's rel. 1e-4 check on every row, y bit-identical to the oracle
+    on a sample of rows."""
+    import oracle
+    n = m = 32768
+    y = tmp_path / "y.f32"
+    rcs, outs = _launch_ranks([_exe("gesummv_smi_host"), "-n", str(n), "-m", str(m), "-a", "1.5", "-c", "0.5",
+                               "-r", "2", "-y", str(y)], 8, tmp_path, timeout=400)
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    assert "OK!!!" in outs[0]
+    got = np.fromfile(y, dtype=np.float32)
+    rows = np.array(sorted({0, 1, 4095, 4096, 16384, 32767} | set(range(7, n, 4099))))
+    A = np.repeat(rows.astype(np.float32)[:, None], m, axis=1)
+    want = oracle.gesummv(A, A, np.ones(m, dtype=np.float32), 1.5, 0.5)
+    assert np.array_equal(got[rows].view(np.uint32), want.view(np.uint32))
