@@ -41,7 +41,10 @@ typedef enum {
  * Schedule: owner-chunk exchange -> canonical rank-order fold on each owner
  * -> gather on the root, pipelined over pieces of smi_set_pipeline_bytes()
  * bytes per owner chunk (the fold of one piece overlaps the exchange of the
- * next).  Results do not depend on the piece size. */
+ * next).  Messages up to 256 KiB (latency-bound) take a direct fan-in
+ * instead: every rank's buffer to the root in one transfer group and one
+ * rank-order fold there.  Results depend on neither the path nor the piece
+ * size: every element is folded over the ranks in rank order. */
 int smi_reduce(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count,
                SMI_Datatype type, SMI_Op op, int root, int port,
                SMI_Stream stream);

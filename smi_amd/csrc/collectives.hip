@@ -11,7 +11,8 @@
 //   reduce = owner-chunk exchange (rank r sends chunk c of its buffer to
 //            owner c) -> canonical rank-order fold on each owner (HIP kernel,
 //            bit-identical to the reference fold with arrival = rank order)
-//            -> owners send their reduced chunk to the root;
+//            -> owners send their reduced chunk to the root (messages up
+//            to 256 KiB: direct fan-in to the root and one fold there);
 //   bcast  = scatter of the root's chunks -> all-gather between the ranks
 //            (small messages: direct fan-out from the root).
 // Every step is a transport group of point-to-point transfers on the
@@ -206,6 +207,10 @@ static size_t chunk_len(size_t count, size_t cs, int c) {
 // pieces of ps elements (a multiple of 16 bytes, so pieces of an aligned
 // buffer stay aligned).  g_piece_bytes = 0: one piece (no pipelining).
 size_t g_piece_bytes = (size_t)4 << 20;
+
+// smi_reduce messages up to this size take the direct fan-in (as smi_bcast's
+// direct fan-out, below): latency, not link bandwidth, bounds them
+constexpr size_t kReduceFanInBytes = (size_t)256 * 1024;
 struct Pieces {
     size_t ps;  // elements per piece
     int n;      // pieces per chunk
@@ -271,6 +276,31 @@ int smi_reduce(SMI_Comm comm, const void *sendbuf, void *recvbuf, size_t count, 
         FoldRows rows{};
         rows.row[0] = sendbuf;
         return launch_fold(rows, recvbuf, 1, count, type, op, s);
+    }
+    if (count * esz <= kReduceFanInBytes) {
+        // Latency-bound: a direct fan-in, all on the caller's stream -- every
+        // rank's whole buffer to the root in one transport group, then one
+        // canonical rank-order fold there: one round instead of the owner
+        // chunks' two (exchange, then gather), and the same fold over the
+        // same rows, so the same bits.
+        if (me != root) {
+            Group grp(c->transport.get());
+            SMI_TRY(grp.begin(s));
+            SMI_TRY(c->transport->send(sendbuf, count * esz, root));
+            return grp.end();
+        }
+        const size_t rst = (count * esz + 15) / 16 * 16;  // staging row stride (16-byte aligned rows)
+        void *ws = nullptr;
+        SMI_TRY(comm_workspace(c, (size_t)n * rst, &ws));
+        FoldRows rows{};
+        Group grp(c->transport.get());
+        SMI_TRY(grp.begin(s));
+        for (int k = 0; k < n; ++k) {
+            rows.row[k] = k == me ? sendbuf : (const void *)((char *)ws + (size_t)k * rst);
+            if (k != me) SMI_TRY(c->transport->recv((char *)ws + (size_t)k * rst, count * esz, k));
+        }
+        SMI_TRY(grp.end());
+        return launch_fold(rows, recvbuf, n, count, type, op, s);
     }
     const size_t cs = chunk_elems(count, n, esz);
     const Pieces pc = pieces_of(cs, esz);

@@ -155,6 +155,22 @@ def test_reduce_pipelined_pieces_bit_identical(gpu, oracle_mod, piece_bytes, pb,
             assert np.array_equal(got.view(np.uint8), oracle_mod.reduce(c, t, 0).view(np.uint8)), (pb, t, count)
 
 
+@pytest.mark.parametrize("n", [2, 5, 8])
+def test_reduce_fan_in_boundary(gpu, oracle_mod, n):
+    """Messages up to 256 KiB take the direct fan-in (every rank's buffer to
+    the root, one fold there), longer ones the owner chunks: both sides of
+    the threshold, for 4- and 8-byte types and every op, give the oracle's
+    canonical rank-order fold bit for bit."""
+    for t, esz in ((1, 4), (3, 8)):
+        for count in ((256 << 10) // esz, (256 << 10) // esz + 1, 3, (256 << 10) // esz - 5):
+            for op in (0, 1, 2):
+                c = _contribs(oracle_mod, n, count, t, seed=count * 3 + n + op)
+                root = (count + op) % n
+                got = _group_reduce(n, list(c), t, op, root)
+                want = oracle_mod.reduce(c, t, op)
+                assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (n, t, count, op)
+
+
 @pytest.mark.parametrize("pb", [0, 16, 4096])
 @pytest.mark.parametrize("n", [3, 8])
 def test_bcast_pipelined_pieces(gpu, piece_bytes, pb, n):
