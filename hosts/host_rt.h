@@ -16,9 +16,10 @@
 //                              bytes to FILE (written beside it and renamed,
 //                              so a reader never sees part of it), the other
 //                              ranks wait for FILE to appear and every rank
-//                              calls smi_init (RCCL).  FILE must not exist
-//                              when the ranks start.  The device defaults to
-//                              R modulo the visible devices.
+//                              calls smi_init (RCCL); rank 0 removes FILE
+//                              once smi_init has returned.  FILE must not
+//                              exist when the ranks start.  The device
+//                              defaults to R modulo the visible devices.
 //
 // MPI_Barrier is restated on the communicator (Barrier below); tiles and
 // results move with smi_scatter / smi_gather where the reference used
@@ -140,6 +141,10 @@ inline int run_ranks(const Launch &l, int ranks, const std::function<int(SMI_Com
         }
         SMI_Comm comm;
         SMI_OK(smi_init(l.rank, l.size, dev, id, SMI_UNIQUE_ID_BYTES, &comm));
+        // smi_init is collective: once it returns every rank has read the
+        // id, so rank 0 removes the file (a later job on the same path then
+        // cannot pick up this job's id)
+        if (l.rank == 0) std::remove(l.uid.c_str());
         const int rc = body(comm);
         SMI_OK(smi_finalize(comm));
         return rc;

@@ -207,6 +207,7 @@ def test_stencil_host_processes_config1_matches_golden(tmp_path, pxpy):
     assert all(rc == 0 for rc in rcs), _log(rcs, outs)
     assert "Successfully verified result." in outs[0]
     assert hashlib.sha256(out.read_bytes()).hexdigest() == _golden_config1()
+    assert not list(tmp_path.glob("uid_*"))  # rank 0 removed the id file after smi_init
 
 
 @pytest.mark.gpu
