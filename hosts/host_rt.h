@@ -39,6 +39,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <initializer_list>
 #include <string>
 #include <thread>
 #include <vector>
@@ -77,10 +78,27 @@ struct Launch {
     bool process() const { return rank >= 0; }
 };
 
-// Takes --rank/--size/--uid/--device out of argv (the host parses the rest).
+inline const char *env_of(std::initializer_list<const char *> names) {
+    for (const char *n : names)
+        if (const char *v = std::getenv(n)) return v;
+    return nullptr;
+}
+
+// Takes --rank/--size/--uid/--device/--fake-host out of argv (the host
+// parses the rest).  Without --rank, a launcher's environment selects the
+// one-process-per-rank mode as mpirun does for the reference's hosts:
+// torchrun (RANK, WORLD_SIZE, LOCAL_RANK; `torchrun --no-python
+// --nproc-per-node 8 hosts/_build/stencil_smi_host ...`), Open MPI
+// (OMPI_COMM_WORLD_*), MPICH / Slurm (PMI_RANK / PMI_SIZE, SLURM_PROCID /
+// SLURM_NTASKS).  The id file then defaults to $TMPDIR/smi_uid.<job>, the
+// job named by MASTER_PORT, SLURM_JOB_ID or the launcher's process id.
+// --fake-host gives every rank its own NCCL_HOSTID (bench.py --fake-host):
+// several ranks on one GPU, RCCL over its socket transport -- testing only.
 // Returns false on a malformed launch.
 inline bool parse_launch(int &argc, char **argv, Launch *l) {
     int out = 1;
+    bool fake_host = false;
+    bool device_given = false;
     for (int i = 1; i < argc; ++i) {
         const std::string k = argv[i];
         if ((k == "--rank" || k == "--size" || k == "--uid" || k == "--device") && i + 1 < argc) {
@@ -88,14 +106,43 @@ inline bool parse_launch(int &argc, char **argv, Launch *l) {
             if (k == "--rank") l->rank = std::atoi(v);
             else if (k == "--size") l->size = std::atoi(v);
             else if (k == "--uid") l->uid = v;
-            else l->device = std::atoi(v);
+            else {
+                l->device = std::atoi(v);
+                device_given = true;
+            }
+        } else if (k == "--fake-host") {
+            fake_host = true;
         } else {
             argv[out++] = argv[i];
         }
     }
     argc = out;
     argv[argc] = nullptr;
+    if (l->rank < 0) {
+        const char *r = env_of({"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID"});
+        const char *n = env_of({"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS"});
+        if (r && n) {
+            l->rank = std::atoi(r);
+            l->size = std::atoi(n);
+            if (l->device < 0)
+                if (const char *lr = env_of({"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID",
+                                             "SLURM_LOCALID"}))
+                    l->device = std::atoi(lr);
+            if (l->uid.empty()) {
+                const char *job = env_of({"MASTER_PORT", "SLURM_JOB_ID"});
+                const char *tmp = env_of({"TMPDIR"});
+                l->uid = std::string(tmp ? tmp : "/tmp") + "/smi_uid." +
+                         (job ? std::string(job) : std::to_string(getppid()));
+            }
+        }
+    }
     if (l->rank >= 0 && (l->size <= 0 || l->rank >= l->size || l->uid.empty())) return false;
+    if (fake_host && l->rank >= 0) {
+        // before the first HIP / RCCL call: RCCL reads it at communicator set-up
+        const std::string id = "smi-fake-host-" + std::to_string(l->rank);
+        setenv("NCCL_HOSTID", id.c_str(), 1);
+        if (!device_given) l->device = 0;  // every rank on GPU 0
+    }
     return true;
 }
 

@@ -84,6 +84,28 @@ def test_hosts_process_mode_fails_loudly_without_gpu(tmp_path):
     assert r.returncode == 1  # a malformed launch is a usage error
 
 
+def test_hosts_take_ranks_from_a_launcher_environment(tmp_path):
+    """Without --rank a launcher's environment (torchrun's RANK / WORLD_SIZE,
+    Open MPI's OMPI_COMM_WORLD_*, PMI_*, SLURM_*) selects one process per
+    rank: with no GPU, rank 0 stops at smi_get_unique_id (exit 2); a rank
+    outside the job is a usage error (exit 1)."""
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is visible: the GPU tests run the hosts")
+    base = {k: v for k, v in os.environ.items()
+            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE",
+                         "PMI_RANK", "PMI_SIZE", "SLURM_PROCID", "SLURM_NTASKS")}
+    args = [_exe("stencil_smi_host"), "256", "256", "1", "2", "32"]
+    for envs in ({"RANK": "0", "WORLD_SIZE": "2", "MASTER_PORT": "29999"},
+                 {"OMPI_COMM_WORLD_RANK": "0", "OMPI_COMM_WORLD_SIZE": "2"},
+                 {"PMI_RANK": "0", "PMI_SIZE": "2"}):
+        r = subprocess.run(args, env=dict(base, TMPDIR=str(tmp_path), **envs), capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 2 and "smi_get_unique_id" in r.stderr, (envs, r.stdout + r.stderr)
+    r = subprocess.run(args, env=dict(base, RANK="3", WORLD_SIZE="2"), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1, r.stdout + r.stderr
+
+
 def _launch_ranks(args, world, tmp_path, timeout=240, stall=None):
     """One process per rank (--rank/--size/--uid), started with subprocess;
     every rank is killed once one fails or the time limit passes.  Returns
@@ -380,3 +402,26 @@ def test_config5_gesummv_32768_8_processes(tmp_path):
     A = np.repeat(rows.astype(np.float32)[:, None], m, axis=1)
     want = oracle.gesummv(A, A, np.ones(m, dtype=np.float32), 1.5, 0.5)
     assert np.array_equal(got[rows].view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_stencil_host_under_torchrun(tmp_path):
+    """The C++ host launched like the reference's (mpirun -np N), here by
+    torchrun --no-python: ranks from RANK / WORLD_SIZE, the id file named by
+    MASTER_PORT, --fake-host for two ranks on one GPU.  BASELINE config 1 as
+    1x2 ranks, bit-identical to the golden hash."""
+    import socket
+    import sys
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    out = tmp_path / "res.f32"
+    env = dict(os.environ, TMPDIR=str(tmp_path), HSA_ENABLE_IPC_MODE_LEGACY="0", NCCL_SOCKET_IFNAME="lo",
+               NCCL_IB_DISABLE="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--no-python", "--nnodes", "1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        _exe("stencil_smi_host"), "256", "256", "1", "2", "32", "--fake-host", "--out", str(out)],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "Successfully verified result." in r.stdout
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == _golden_config1()
