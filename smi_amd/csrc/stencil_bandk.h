@@ -297,14 +297,32 @@ struct BandL {
     // (((S + W) + E) + N) each).  ROWWALK: cells = columns (a | b), W / E of
     // a = b of lane-1 / own b, of b = own a / a of lane+1; else cells = rows,
     // N / S of a = b of lane-1 / own b, of b = own a / a of lane+1.
+    // The two cells' adds are scalar where an operand crosses lanes (DPP,
+    // fused into the add) and packed (v_pk_add_f32) where both operands are
+    // a lane's own register pair; the x 0.25 is one v_pk_mul_f32: 6 VALU per
+    // lane-level instead of 8, the same IEEE operations in the same order.
     template <bool ROWWALK>
     __device__ __forceinline__ static float2 cell2(float2 older, float2 c, float2 newer) {
-        if constexpr (ROWWALK)
-            return make_float2(jacobi(newer.x, shr1_any(c.y), c.y, older.x),
-                               jacobi(newer.y, c.x, shl1_any(c.x), older.y));
-        else
-            return make_float2(jacobi(c.y, older.x, newer.x, shr1_any(c.y)),
-                               jacobi(shl1_any(c.x), older.y, newer.y, c.x));
+        const f32x2 q = {0.25f, 0.25f};
+        if constexpr (ROWWALK) {
+            // ((S + W) + E) per cell, then + N on the pair
+            float a = __fadd_rn(__fadd_rn(newer.x, shr1_any(c.y)), c.y);
+            float b = __fadd_rn(__fadd_rn(newer.y, c.x), shl1_any(c.x));
+            asm("" : "+v"(a), "+v"(b));  // no re-pairing of the scalar adds (moves)
+            const f32x2 o = (f32x2{a, b} + f32x2{older.x, older.y}) * q;
+            return make_float2(o.x, o.y);
+        } else {
+            // (S + W) per cell, + E on the pair, + N per cell
+            float a = __fadd_rn(c.y, older.x);
+            float b = __fadd_rn(shl1_any(c.x), older.y);
+            asm("" : "+v"(a), "+v"(b));
+            const f32x2 p = f32x2{a, b} + f32x2{newer.x, newer.y};
+            float u = __fadd_rn(p.x, shr1_any(c.y));
+            float v = __fadd_rn(p.y, c.x);
+            asm("" : "+v"(u), "+v"(v));
+            const f32x2 o = f32x2{u, v} * q;
+            return make_float2(o.x, o.y);
+        }
     }
 
     // Levels 1..LV over N inputs: ld(t) yields input t (issuing its own
