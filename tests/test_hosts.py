@@ -48,8 +48,20 @@ def _exe(name):
     return path
 
 
+# a launcher's variables select the hosts' one-process-per-rank mode
+# (hosts/host_rt.h): the threads-mode runs start without them
+_LAUNCHER_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE",
+                  "OMPI_COMM_WORLD_LOCAL_RANK", "PMI_RANK", "PMI_SIZE", "SLURM_PROCID", "SLURM_NTASKS")
+
+
+def _clean_env(**extra):
+    env = {k: v for k, v in os.environ.items() if k not in _LAUNCHER_VARS}
+    env.update(extra)
+    return env
+
+
 def _run(args, timeout=120):
-    return subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+    return subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=_clean_env())
 
 
 def test_hosts_build_and_fail_loudly_without_gpu():
@@ -92,9 +104,7 @@ def test_hosts_take_ranks_from_a_launcher_environment(tmp_path):
     import torch
     if torch.cuda.device_count() > 0:
         pytest.skip("a GPU is visible: the GPU tests run the hosts")
-    base = {k: v for k, v in os.environ.items()
-            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE",
-                         "PMI_RANK", "PMI_SIZE", "SLURM_PROCID", "SLURM_NTASKS")}
+    base = _clean_env()
     args = [_exe("stencil_smi_host"), "256", "256", "1", "2", "32"]
     for envs in ({"RANK": "0", "WORLD_SIZE": "2", "MASTER_PORT": "29999"},
                  {"OMPI_COMM_WORLD_RANK": "0", "OMPI_COMM_WORLD_SIZE": "2"},
@@ -117,7 +127,7 @@ def _launch_ranks(args, world, tmp_path, timeout=240, stall=None):
     uid = tmp_path / f"uid_{world}_{time.monotonic_ns()}"
     procs = []
     for r in range(world):
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = _clean_env(HSA_ENABLE_IPC_MODE_LEGACY="0")
         if ngpu < world:
             env.update(NCCL_HOSTID=f"smi-host-test-{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
         procs.append(subprocess.Popen(args + ["--rank", str(r), "--size", str(world), "--uid", str(uid)], env=env,
@@ -416,8 +426,8 @@ def test_stencil_host_under_torchrun(tmp_path):
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     out = tmp_path / "res.f32"
-    env = dict(os.environ, TMPDIR=str(tmp_path), HSA_ENABLE_IPC_MODE_LEGACY="0", NCCL_SOCKET_IFNAME="lo",
-               NCCL_IB_DISABLE="1")
+    env = _clean_env(TMPDIR=str(tmp_path), HSA_ENABLE_IPC_MODE_LEGACY="0", NCCL_SOCKET_IFNAME="lo",
+                     NCCL_IB_DISABLE="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--no-python", "--nnodes", "1",
                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", str(port),
                         _exe("stencil_smi_host"), "256", "256", "1", "2", "32", "--fake-host", "--out", str(out)],

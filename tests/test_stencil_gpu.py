@@ -658,6 +658,50 @@ def test_scaled_guard_fuzz(gpu, oracle_mod, seed):
     assert np.array_equal(bits(_run_fused(g, T, k=k)), bits(oracle_mod.stencil(g, T))), (X, Y, k, T)
 
 
+@pytest.mark.parametrize("k", [13, 16, 20])
+@pytest.mark.parametrize("pxpy", [(2, 2), (1, 3), (3, 1)])
+def test_band_special_values(gpu, oracle_mod, k, pxpy):
+    """Decomposed K >= 13 passes (the lean band kernel beside the rotating-ring
+    interior, whose waves walk scaled levels under their input guard) on
+    tiles salted with signed zeros, subnormals, the largest finite values,
+    infinities and NaN, which also reach the bands through the halos:
+    bit-exact (NaN payloads aside) vs the oracle."""
+    PX, PY = pxpy
+    g = _special_grid(6 * k + 20 * PX, 268 * PY, seed=k * 5 + PX)
+    for T in (k, 2 * k + 3):
+        got = _run_fused(g, T, PX, PY, k=k)
+        assert _same(got, oracle_mod.stencil(g, T)), (k, pxpy, T)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_band_scaled_guard_fuzz(gpu, oracle_mod, seed):
+    """Decomposed tiles with patches of magnitudes 2^-135 .. 2^110 (mixed
+    signs, zeros) straddling the internal tile boundaries -- the band
+    kernel's inputs and the halos -- so that within one pass some interior
+    waves pass the scaled-level guard and others walk exactly next to the
+    band kernel's exact walks; K = 13..20, bit-exact vs the oracle."""
+    rng = np.random.default_rng(500 + seed)
+    PX, PY = [(2, 2), (1, 2), (2, 1), (3, 2), (2, 3), (1, 3), (3, 1), (2, 2)][seed]
+    k = int(rng.integers(13, 21))
+    xl = 6 * k + int(rng.integers(0, 60))
+    yl = 4 * int(rng.integers(40, 90))
+    X, Y = xl * PX, yl * PY
+    g = rng.random((X, Y), dtype=np.float32)
+    bounds = [(r, None) for r in range(xl, X, xl)] + [(None, c) for c in range(yl, Y, yl)]
+    for _ in range(int(rng.integers(3, 8))):
+        br, bc = bounds[int(rng.integers(0, len(bounds)))]
+        r0 = (br - int(rng.integers(0, 2 * k))) if br is not None else int(rng.integers(0, X - 8))
+        c0 = (bc - int(rng.integers(0, 2 * k))) if bc is not None else int(rng.integers(0, Y - 8))
+        r0, c0 = max(r0, 0), max(c0, 0)
+        h, w = int(rng.integers(1, 3 * k)), int(rng.integers(1, 3 * k))
+        e = rng.integers(-135, 111, size=(min(h, X - r0), min(w, Y - c0)))
+        sgn = rng.choice(np.array([-1.0, 1.0, 0.0], np.float32), size=e.shape, p=[0.45, 0.45, 0.1])
+        g[r0:r0 + h, c0:c0 + w] = (sgn * np.ldexp(rng.random(e.shape) + 0.5, e)).astype(np.float32)
+    T = int(rng.integers(k, 2 * k + 3))
+    got = _run_fused(g, T, PX, PY, k=k)
+    assert np.array_equal(bits(got), bits(oracle_mod.stencil(g, T))), (PX, PY, xl, yl, k, T)
+
+
 def test_profiling_entries_distinct(gpu, oracle_mod):
     """smi_prof_list counts distinct (kernel, tag) pairs, also for the
     max_entries = 0 size query profiling.entries() starts with: a 41-step
