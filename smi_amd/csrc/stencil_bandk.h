@@ -289,7 +289,13 @@ struct BandL {
     static constexpr int KS = (K + LMAX - 1) / LMAX;
     static constexpr int lv(int s) { return K / KS + (s < K % KS ? 1 : 0); }
     static constexpr int L0 = lv(0);
-    static constexpr int NPOS = (NR > NC ? NR : NC) - 2 * L0;  // parked positions (x 2 cells) per lane
+    // parked positions (x 2 cells) per lane: a row walk's stage outputs, or
+    // a column walk's staged inputs (its 3KC columns, float4 groups from
+    // -KC / Y - 2KC) -- whichever is more
+    static constexpr int NPOS = (NR - 2 * L0 > 3 * KC) ? NR - 2 * L0 : 3 * KC;
+    // LDS stride of one position, in float2: 64 lanes + 1, so that the
+    // transposing writes of the column walks' staging spread over the banks
+    static constexpr int PST = 65;
     static constexpr int LA = 3;                                // global inputs loaded ahead
     static constexpr int LAS = 2;                               // parked values read ahead
 
@@ -366,16 +372,16 @@ struct BandL {
         // them all in registers (and spills)
         asm volatile("" ::: "memory");
         float2 y[N];
-        static_for<LAS>([&](auto U) { y[U] = park[U * 64 + lane]; });
+        static_for<LAS>([&](auto U) { y[U] = park[U * PST + lane]; });
         auto ld = [&](auto U) {
             constexpr int u = U;
-            if constexpr (u + LAS < N) y[u + LAS] = park[(u + LAS) * 64 + lane];
+            if constexpr (u + LAS < N) y[u + LAS] = park[(u + LAS) * PST + lane];
             return y[u];
         };
         if constexpr (S + 1 == KS) {
             walk<ROWWALK, CP, N, LV>(cpa, cpb, ld, out);
         } else {
-            walk<ROWWALK, CP, N, LV>(cpa, cpb, ld, [&](auto U, float2 v) { park[U * 64 + lane] = v; });
+            walk<ROWWALK, CP, N, LV>(cpa, cpb, ld, [&](auto U, float2 v) { park[U * PST + lane] = v; });
             stages<ROWWALK, CP, S + 1, N - 2 * LV>(cpa, cpb, park, lane, out);
         }
     }
@@ -413,7 +419,7 @@ struct BandL {
                 if constexpr (t + LA < NR) x[t + LA] = gload(std::integral_constant<int, t + LA>{});
                 return x[t];
             },
-            [&](auto U, float2 v) { park[U * 64 + lane] = v; });
+            [&](auto U, float2 v) { park[U * PST + lane] = v; });
         const int KCr = a.kc;
         stages<true, CP, 1, NR - 2 * L0>(cpa, cpb, park, lane, [&](auto Q, float2 v) {
             constexpr int q = Q;  // output row r0 + K + q
@@ -433,63 +439,80 @@ struct BandL {
         });
     }
 
-    // left (RIGHT = false) or right band: lane = rows r, r + 1, columns c0 + t
+    // left (RIGHT = false) or right band: lane = rows r, r + 1, columns c0 + t.
+    // The walk is transposed (a lane owns two rows), but its global memory
+    // traffic is not: the wave's 128 rows x 3KC input columns are loaded
+    // row-contiguously (float4 groups, consecutive lanes along a row) and
+    // written transposed into its LDS park, the walk reads its inputs from
+    // there, and the KC output columns leave through the park the same way.
+    // Lanes reading / writing 64 different rows per instruction made the
+    // interior sweep beside this kernel ~7 % slower per pass than the row walks
+    // with the same arithmetic (rehearsal cases brows / bcols, DESIGN.md
+    // section 6).
     template <bool RIGHT, bool CP>
     __device__ __forceinline__ static void cols(const BandKArgs &a, int w, int lane, float2 *park) {
         const int X = a.rows, Y = a.cols;
-        const int r = a.rlo + w * SW - KE + 2 * lane;
+        const int R = a.rlo + w * SW - KE;  // the wave's first row; lane l walks rows R + 2l, R + 2l + 1
+        const int r = R + 2 * lane;
         const int g0 = RIGHT ? Y - 2 * KC : -KC;
         const BandSrc src(a, K);
-        // per row two contiguous runs: left band: halo columns [-KC, 0) then
-        // tile columns [0, 2KC); right band: tile [Y-2KC, Y) then halo
-        // [Y, Y+KC) (a band exists only beside a neighbour)
-        constexpr int JB = RIGHT ? 2 * KC / 4 : KC / 4;  // first group of the second run
-        const float *pa0 = src.at(r, g0), *pb0 = src.at(r, g0 + 4 * JB);
-        const float *pa1 = src.at(r + 1, g0), *pb1 = src.at(r + 1, g0 + 4 * JB);
-        auto ldg = [&](auto J, const float *pa, const float *pb) {
-            constexpr int j = J;
-            return *reinterpret_cast<const float4 *>(j < JB ? pa + 4 * j : pb + 4 * (j - JB));
-        };
-        constexpr int E0 = KC - K;  // walk input t is element E0 + t of the groups
-        const bool store = lane >= KE / 2 && lane < 64 - KE / 2;
-        const bool st0 = store && r < a.rhi, st1 = store && r + 1 < a.rhi;
+        float *pf = reinterpret_cast<float *>(park);
+        // staging: element e in [0, 3KC) of row R + rho -> park[e][rho / 2] . (rho % 2)
+        constexpr int NG = 3 * KC / 4;  // float4 groups per row
+        constexpr int NI = (128 * NG + 63) / 64, IB = 6;  // instructions, in batches of IB loads in flight
+#pragma unroll 1
+        for (int i0 = 0; i0 < NI; i0 += IB) static_for<IB>([&](auto I) {
+            const int idx = (i0 + (int)I) * 64 + lane;
+            if (idx < 128 * NG) {
+                const int rho = idx / NG, j = idx - rho * NG;
+                const float4 q = *reinterpret_cast<const float4 *>(src.at(R + rho, g0 + 4 * j));
+                float *d = pf + ((4 * j) * PST + (rho >> 1)) * 2 + (rho & 1);
+                d[0] = q.x;
+                d[2 * PST] = q.y;
+                d[4 * PST] = q.z;
+                d[6 * PST] = q.w;
+            }
+        });
+        asm volatile("" ::: "memory");  // (the walk reads the staging back)
+        constexpr int E0 = KC - K;      // walk input t is staged element E0 + t
         const bool cpa = (!a.has[0] && r == 0) || (!a.has[1] && r == X - 1);
         const bool cpb = (!a.has[0] && r + 1 == 0) || (!a.has[1] && r + 1 == X - 1);
-        float4 g0r[G4], g1r[G4];
-        auto fetch = [&](auto J) {
-            g0r[J] = ldg(J, pa0, pb0);
-            g1r[J] = ldg(J, pa1, pb1);
-        };
-        fetch(std::integral_constant<int, E0 / 4>{});
-        auto comp = [](const float4 &q4, int e) { return e == 0 ? q4.x : e == 1 ? q4.y : e == 2 ? q4.z : q4.w; };
+        float2 y[LAS + 1];
+        static_for<LAS>([&](auto U) { y[U] = park[(E0 + U) * PST + lane]; });
         walk<false, CP, NC, L0>(
             cpa, cpb,
             [&](auto T) {
-                constexpr int t = T, e = E0 + t;
-                // entering group e/4: fetch the next (two rows x 4 floats
-                // per group in flight: the 64-VGPR budget)
-                if constexpr (e % 4 == 0 || t == 0)
-                    if constexpr (e / 4 + 1 < G4) fetch(std::integral_constant<int, e / 4 + 1>{});
-                return make_float2(comp(g0r[e / 4], e % 4), comp(g1r[e / 4], e % 4));
+                constexpr int t = T;
+                if constexpr (t + LAS < NC) y[(t + LAS) % (LAS + 1)] = park[(E0 + t + LAS) * PST + lane];
+                return y[t % (LAS + 1)];
             },
-            [&](auto U, float2 v) { park[U * 64 + lane] = v; });
+            [&](auto U, float2 v) { park[U * PST + lane] = v; });
+        // the last stage's KC outputs into park[0 .. KC), then out row-contiguously
+        stages<false, CP, 1, NC - 2 * L0>(cpa, cpb, park, lane, [&](auto Q, float2 v) { park[Q * PST + lane] = v; });
+        asm volatile("" ::: "memory");
         const int c0 = RIGHT ? Y - KC : 0;
         float *send = RIGHT ? a.h.send_right : a.h.send_left;
-        float2 o[4];
-        auto put = [&](int rr, float4 vv, int j) {
-            *reinterpret_cast<float4 *>(a.out + (size_t)rr * Y + c0 + j) = vv;
-            if (!a.pack) return;
-            *reinterpret_cast<float4 *>(send + (size_t)rr * KC + j) = vv;
-            if (rr < K) *reinterpret_cast<float4 *>(a.h.send_corner[RIGHT ? 1 : 0] + rr * KC + j) = vv;
-            if (rr >= X - K) *reinterpret_cast<float4 *>(a.h.send_corner[RIGHT ? 3 : 2] + (rr - (X - K)) * KC + j) = vv;
-        };
-        stages<false, CP, 1, NC - 2 * L0>(cpa, cpb, park, lane, [&](auto Q, float2 v) {
-            constexpr int q = Q;  // output column c0 + q
-            o[q % 4] = v;
-            if constexpr (q % 4 == 3) {
-                constexpr int j = q - 3;
-                if (st0) put(r, make_float4(o[0].x, o[1].x, o[2].x, o[3].x), j);
-                if (st1) put(r + 1, make_float4(o[0].y, o[1].y, o[2].y, o[3].y), j);
+        constexpr int NO = KC / 4;  // float4 groups of a row's outputs
+        constexpr int NJ = (128 * NO + 63) / 64;
+#pragma unroll 1
+        for (int i0 = 0; i0 < NJ; i0 += IB) static_for<IB>([&](auto I) {
+            const int idx = (i0 + (int)I) * 64 + lane;
+            if (idx < 128 * NO) {
+                const int rho = idx / NO, j = idx - rho * NO;
+                const int rr = R + rho;
+                if (rho >= KE && rho < 128 - KE && rr < a.rhi) {
+                    const float *sv = pf + ((4 * j) * PST + (rho >> 1)) * 2 + (rho & 1);
+                    const float4 v = make_float4(sv[0], sv[2 * PST], sv[4 * PST], sv[6 * PST]);
+                    *reinterpret_cast<float4 *>(a.out + (size_t)rr * Y + c0 + 4 * j) = v;
+                    if (a.pack) {
+                        *reinterpret_cast<float4 *>(send + (size_t)rr * KC + 4 * j) = v;
+                        // corner blocks of rows this band owns (only when the top /
+                        // bottom side is a global edge, i.e. never sent)
+                        if (rr < K) *reinterpret_cast<float4 *>(a.h.send_corner[RIGHT ? 1 : 0] + rr * KC + 4 * j) = v;
+                        if (rr >= X - K)
+                            *reinterpret_cast<float4 *>(a.h.send_corner[RIGHT ? 3 : 2] + (rr - (X - K)) * KC + 4 * j) = v;
+                    }
+                }
             }
         });
     }
@@ -529,15 +552,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     // living on the interior's leftover issue slots until its end
     __builtin_amdgcn_s_setprio(3);
     extern __shared__ float2 bandl_lds[];
-    float2 *park = bandl_lds + (threadIdx.x >> 6) * (BandL<K>::NPOS * 64);
+    float2 *park = bandl_lds + (threadIdx.x >> 6) * (BandL<K>::NPOS * BandL<K>::PST);
     for (int wv = wv0; wv < a.first[4]; wv += waves)  // wave-uniform
         bandl_wave<K>(a, wv, threadIdx.x & 63, park);
 }
 
 // LDS each lean workgroup reserves: more than half of the CU's 160 KiB (its
-// four waves park 4 x NPOS x 64 float2 in it: 100 KiB at K = 20)
-constexpr int kBandLeanLds = 100 * 1024;
-static_assert(4 * BandL<SWEEPD_MAX>::NPOS * 64 * 8 <= kBandLeanLds, "lean band kernel: LDS park too small");
+// four waves park 4 x NPOS x PST float2 in it: 121.9 KiB at K = 20)
+constexpr int kBandLeanLds = 122 * 1024;
+static_assert(4 * BandL<SWEEPD_MAX>::NPOS * BandL<SWEEPD_MAX>::PST * 8 <= kBandLeanLds,
+              "lean band kernel: LDS park too small");
+static_assert(kBandLeanLds > 80 * 1024 && kBandLeanLds <= 160 * 1024, "one lean workgroup per CU");
 
 template <int K>
 int bandl_launch_impl(const BandKArgs &a, int blocks, hipStream_t s, hipEvent_t start, hipEvent_t stop) {

@@ -85,8 +85,19 @@ int plan_bands(int K, BandKArgs *ap, bool lean) {
     }
     a.first[4] = n;
 #ifdef SMI_LOOPBACK_REHEARSAL
-    // timing experiment: no band work at all (results are wrong)
+    // timing experiments (results are wrong): no band work at all, or only
+    // the row walks (top / bottom bands) or only the transposed column walks
     if (getenv("SMI_REH_NOBANDS")) a.first[1] = a.first[2] = a.first[3] = a.first[4] = 0;
+    if (const char *m = getenv("SMI_REH_BANDS")) {
+        if (m[0] == 'r') {
+            a.first[3] = a.first[4] = a.first[2];
+        } else if (m[0] == 'c') {
+            const int nl = a.first[3] - a.first[2], nr = a.first[4] - a.first[3];
+            a.first[1] = a.first[2] = 0;
+            a.first[3] = nl;
+            a.first[4] = nl + nr;
+        }
+    }
 #endif
     return SMI_SUCCESS;
 }

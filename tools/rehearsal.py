@@ -16,6 +16,8 @@ run by run so that clock drift hits every case alike):
   bands  -- interior rank without the exchange (SMI_LOOPBACK_NOXCHG)
   xchg   -- interior rank without the band work (SMI_REH_NOBANDS)
   bare   -- neither: the two-stream schedule and the host join only
+  brows / bcols -- bands without the exchange, only the top / bottom row
+           walks or only the transposed left / right column walks
 The exchange is RCCL's real kernel by default (a one-rank RCCL communicator
 whose 8 sends and receives per pass go to itself through the production
 RcclTransport); REHEARSAL_TRANSPORT=local uses the in-process transport.
@@ -51,8 +53,11 @@ CASES = {
     "bands": {"SMI_LOOPBACK": "1", "SMI_LOOPBACK_NOXCHG": "1"},
     "xchg": {"SMI_LOOPBACK": "1", "SMI_REH_NOBANDS": "1"},
     "bare": {"SMI_LOOPBACK": "1", "SMI_LOOPBACK_NOXCHG": "1", "SMI_REH_NOBANDS": "1"},
+    # the band kernel's two halves, no exchange
+    "brows": {"SMI_LOOPBACK": "1", "SMI_LOOPBACK_NOXCHG": "1", "SMI_REH_BANDS": "rows"},
+    "bcols": {"SMI_LOOPBACK": "1", "SMI_LOOPBACK_NOXCHG": "1", "SMI_REH_BANDS": "cols"},
 }
-SWITCHES = ("SMI_LOOPBACK", "SMI_LOOPBACK_NOXCHG", "SMI_REH_NOBANDS")
+SWITCHES = ("SMI_LOOPBACK", "SMI_LOOPBACK_NOXCHG", "SMI_REH_NOBANDS", "SMI_REH_BANDS")
 
 
 def set_case(name):
