@@ -126,20 +126,24 @@ def stencil_cases(comm, rank, world, s):
                     got = stencil.combine_memory(out, PX, PY)
                     report(rank, f"stencil {PX}x{PY} T={T} overlap={overlap} K={fuse}",
                            np.array_equal(got.view(np.uint32), want.view(np.uint32)))
-    # three K = 20 passes: the host-observed pass join between passes over RCCL
+    # three K = 20 passes over RCCL, the pass boundary joined on the host
+    # (default) and by a device-side stream wait (smi_stencil_set_join(0))
     T = 60
     want = oracle.stencil(g, T) if rank == 0 else None
     stencil.set_tuning(overlap=1)
     stencil.set_fusion(steps_per_pass=20)
-    t = torch.from_numpy(tiles[rank]).cuda()
-    res = stencil.run(comm, t, T, PX, PY)
-    s.synchronize()
-    out = [None] * world
-    dist.all_gather_object(out, res.cpu().numpy())
-    if rank == 0:
-        got = stencil.combine_memory(out, PX, PY)
-        report(rank, f"stencil {PX}x{PY} T={T} overlap=1 K=20 (three passes)",
-               np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+    for join in (1, 0):
+        stencil.set_join(join)
+        t = torch.from_numpy(tiles[rank]).cuda()
+        res = stencil.run(comm, t, T, PX, PY)
+        s.synchronize()
+        out = [None] * world
+        dist.all_gather_object(out, res.cpu().numpy())
+        if rank == 0:
+            got = stencil.combine_memory(out, PX, PY)
+            report(rank, f"stencil {PX}x{PY} T={T} overlap=1 K=20 (three passes) join={join}",
+                   np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+    stencil.set_join(1)
     stencil.set_tuning(overlap=1)
     stencil.set_fusion(steps_per_pass=20)
 
