@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     // band waves first: beside the interior's two waves per SIMD the bands
     // (and the exchange behind them) finish early in the pass instead of
     // living on the interior's leftover issue slots until its end
-    __builtin_amdgcn_s_setprio(3);
+    if (a.prio) __builtin_amdgcn_s_setprio(3);
     extern __shared__ float2 bandl_lds[];
     float2 *park = bandl_lds + (threadIdx.x >> 6) * (BandL<K>::NPOS * BandL<K>::PST);
     for (int wv = wv0; wv < a.first[4]; wv += waves)  // wave-uniform

@@ -84,7 +84,9 @@ int plan_bands(int K, BandKArgs *ap, bool lean) {
         n += waves_of[k];
     }
     a.first[4] = n;
+    a.prio = 1;
 #ifdef SMI_LOOPBACK_REHEARSAL
+    if (const char *v = getenv("SMI_REH_BAND_PRIO")) a.prio = atoi(v) != 0;  // priority A/B
     // timing experiments (results are wrong): no band work at all, or only
     // the row walks (top / bottom bands) or only the transposed column walks
     if (getenv("SMI_REH_NOBANDS")) a.first[1] = a.first[2] = a.first[3] = a.first[4] = 0;

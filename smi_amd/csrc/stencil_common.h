@@ -203,6 +203,7 @@ struct BandKArgs {
     int first[5];      // first wave of band top, bottom, left, right; first[4] = all waves
     int sw;            // cells stored per wave (64 - 2K; lean kernel 128 - 2 KE)
     int rlo, rhi;      // rows of the left/right bands
+    int prio;          // lean kernel: 1 = raised wave priority (s_setprio 3), 0 = normal
 };
 int plan_bands(int K, BandKArgs *a, bool lean);  // fills kc, first[], sw, rlo, rhi
 // the bands of a pass: one wave per segment, or max_waves (> 0) waves;

@@ -18,6 +18,7 @@ run by run so that clock drift hits every case alike):
   bare   -- neither: the two-stream schedule and the host join only
   brows / bcols -- bands without the exchange, only the top / bottom row
            walks or only the transposed left / right column walks
+  full_p0 -- full, the band kernel's waves at normal priority
 The exchange is RCCL's real kernel by default (a one-rank RCCL communicator
 whose 8 sends and receives per pass go to itself through the production
 RcclTransport); REHEARSAL_TRANSPORT=local uses the in-process transport.
@@ -56,8 +57,10 @@ CASES = {
     # the band kernel's two halves, no exchange
     "brows": {"SMI_LOOPBACK": "1", "SMI_LOOPBACK_NOXCHG": "1", "SMI_REH_BANDS": "rows"},
     "bcols": {"SMI_LOOPBACK": "1", "SMI_LOOPBACK_NOXCHG": "1", "SMI_REH_BANDS": "cols"},
+    # the band kernel at the interior's wave priority instead of a raised one
+    "full_p0": {"SMI_LOOPBACK": "1", "SMI_REH_BAND_PRIO": "0"},
 }
-SWITCHES = ("SMI_LOOPBACK", "SMI_LOOPBACK_NOXCHG", "SMI_REH_NOBANDS", "SMI_REH_BANDS")
+SWITCHES = ("SMI_LOOPBACK", "SMI_LOOPBACK_NOXCHG", "SMI_REH_NOBANDS", "SMI_REH_BANDS", "SMI_REH_BAND_PRIO")
 
 
 def set_case(name):
