@@ -213,7 +213,8 @@ def build_hosts(force: bool = False, verbose: bool = False) -> list[str]:
     for src in sorted(glob.glob(os.path.join(HOSTS_DIR, "*.cpp"))):
         exe = os.path.join(out_dir, os.path.splitext(os.path.basename(src))[0])
         outs.append(exe)
-        cmd = [hipcc, "-O2", "-std=c++17", "-Wall", f"-I{os.path.join(ROOT, 'include')}", src, "-o", exe,
+        cmd = [hipcc, "-O2", "-std=c++17", "-Wall", f"--offload-arch={ARCH}", f"-I{os.path.join(ROOT, 'include')}",
+               src, "-o", exe,
                f"-L{OUT_DIR}", "-lsmi_amd", "-lpthread", "-Wl,-rpath,$ORIGIN/../../smi_amd/_build",
                f"-Wl,-rpath,{ROCM}/lib"]
         h = hashlib.sha256(lib_hash.encode())

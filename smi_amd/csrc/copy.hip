@@ -5,7 +5,9 @@
 // exchange of an interior rank is 8 messages per pass, and per-message host
 // calls (copy + events) cost more host time than the pass itself
 // (profiles/r03/).  Segments whose pointers or sizes are not 16-byte
-// multiples go through hipMemcpyAsync.
+// multiples go through hipMemcpyAsync.  Bulk point-to-point messages of the
+// in-process transport (smi_send / smi_recv, hosts/bandwidth_benchmark) are
+// copied by the same kernel.
 #include "smi_internal.h"
 
 namespace smi {
@@ -26,9 +28,16 @@ __global__ __launch_bounds__(256) void multicopy_kernel(CopySegs c, int nseg) {
     const int nb = c.first_block[seg + 1] - b0;
     const uint4 *src = c.src[seg];
     uint4 *dst = c.dst[seg];
-    const unsigned long long n = c.n16[seg];
-    for (unsigned long long i = (unsigned long long)(b - b0) * 256 + threadIdx.x; i < n; i += (unsigned long long)nb * 256)
-        dst[i] = src[i];
+    const unsigned long long n = c.n16[seg], S = (unsigned long long)nb * 256;
+    unsigned long long i = (unsigned long long)(b - b0) * 256 + threadIdx.x;
+    for (; i + 3 * S < n; i += 4 * S) {  // four loads in flight before the stores
+        const uint4 a0 = src[i], a1 = src[i + S], a2 = src[i + 2 * S], a3 = src[i + 3 * S];
+        dst[i] = a0;
+        dst[i + S] = a1;
+        dst[i + 2 * S] = a2;
+        dst[i + 3 * S] = a3;
+    }
+    for (; i < n; i += S) dst[i] = src[i];
 }
 
 #ifdef SMI_LOOPBACK_REHEARSAL
@@ -93,7 +102,9 @@ int launch_copies(const void *const *src, void *const *dst, const size_t *bytes,
         c.dst[nseg] = reinterpret_cast<uint4 *>(dst[i]);
         c.n16[nseg] = n16;
         c.first_block[nseg] = blocks;
-        blocks += (int)std::min<size_t>(256, std::max<size_t>(1, (n16 + 1023) / 1024));  // ~4 vectors per thread
+        // ~4 vectors per thread; a large message gets up to 8 workgroups per
+        // CU (a halo of 16-32 KiB gets one or two)
+        blocks += (int)std::min<size_t>(2048, std::max<size_t>(1, (n16 + 1023) / 1024));
         if (++nseg == kCopyMaxSegs) SMI_TRY(flush());
     }
     return flush();

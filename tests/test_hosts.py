@@ -14,6 +14,10 @@ programs restated without Python in the loop.
   element i == i), bulk smi_bcast and the per-element SMI_Bcast API.
 * hosts/gesummv_smi_host.cpp -- examples/host/gesummv_smi.cpp:48-351: the
   A = B = i, x = 1 pattern, smi_gesummv row-sharded, the rel. 1e-4 check.
+* hosts/bandwidth_benchmark.cpp / latency_benchmark.cpp -- the point-to-point
+  microbenchmarks (microbenchmarks/host/{bandwidth,latency}_benchmark.cpp with
+  kernels/{bandwidth,latency}_{0,1}.cl): two ports of n doubles 0.1f + i, and
+  an int ping-pong incremented on every round trip; element and bulk forms.
 
 Every host runs its ranks either as threads of one process (in-process
 group) or as one process per rank (--rank/--size/--uid, smi_init over RCCL,
@@ -76,7 +80,9 @@ def test_hosts_build_and_fail_loudly_without_gpu():
     for args in ([_exe("stencil_smi_host"), "256", "256", "2", "2", "32"],
                  [_exe("reduce_benchmark"), "-n", "16", "-r", "0", "-i", "1", "-p", "2"],
                  [_exe("broadcast_benchmark"), "-n", "16", "-r", "0", "-i", "1", "-p", "2"],
-                 [_exe("gesummv_smi_host"), "-n", "64", "-m", "64", "-a", "1", "-c", "1", "-r", "1"]):
+                 [_exe("gesummv_smi_host"), "-n", "64", "-m", "64", "-a", "1", "-c", "1", "-r", "1"],
+                 [_exe("bandwidth_benchmark"), "-k", "1", "-r", "1", "-i", "1"],
+                 [_exe("latency_benchmark"), "-n", "4", "-r", "1", "-i", "1"]):
         r = _run(args)
         assert r.returncode == 2, r.stdout + r.stderr
         assert "no GPU visible" in r.stderr
@@ -435,3 +441,39 @@ def test_stencil_host_under_torchrun(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "Successfully verified result." in r.stdout
     assert hashlib.sha256(out.read_bytes()).hexdigest() == _golden_config1()
+
+
+# ------------------------------------------------ point-to-point microbenchmarks --
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,kb,ranks,recv", [("bulk", 4096, 2, 1), ("bulk", 64, 3, 2), ("element", 16, 2, 1)])
+def test_bandwidth_benchmark_host(tmp_path, mode, kb, ranks, recv):
+    """bandwidth_0/1.cl: two ports of doubles 0.1f + i from rank 0 to the
+    receiver, every element checked every run; threads as ranks."""
+    dat = tmp_path / "bw.dat"
+    r = _run([_exe("bandwidth_benchmark"), "-k", str(kb), "-r", str(recv), "-i", "3", "-p", str(ranks), "-m", mode,
+              "-o", str(dat)])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("Result is Ok!") == 3 and "Average bandwidth (Gbit/s)" in r.stdout
+    assert dat.read_text().startswith("#SMI Bandwidth")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,n,ranks,recv", [("element", 200, 2, 1), ("element", 50, 3, 2), ("bulk", 100, 2, 1)])
+def test_latency_benchmark_host(tmp_path, mode, n, ranks, recv):
+    """latency_0/1.cl: an int ping-pong incremented on every round trip,
+    checked on rank 0 every run; threads as ranks."""
+    r = _run([_exe("latency_benchmark"), "-n", str(n), "-r", str(recv), "-i", "3", "-p", str(ranks), "-m", mode])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("Result is Ok!") == 3 and "One-way latency (usec)" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("host,args", [("bandwidth_benchmark", ["-k", "1024", "-r", "1", "-i", "3"]),
+                                       ("bandwidth_benchmark", ["-k", "8", "-r", "1", "-i", "2", "-m", "element"]),
+                                       ("latency_benchmark", ["-n", "100", "-r", "1", "-i", "3"]),
+                                       ("latency_benchmark", ["-n", "50", "-r", "1", "-i", "2", "-m", "bulk"])])
+def test_p2p_benchmarks_processes(tmp_path, host, args):
+    """The same over RCCL with one process per rank."""
+    rcs, outs = _launch_ranks([_exe(host)] + args, 2, tmp_path)
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    assert sum(o.count("Result is Ok!") for o in outs) == int(args[args.index("-i") + 1])
