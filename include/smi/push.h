@@ -3,7 +3,7 @@
  *
  * Same names and argument meaning as the reference include/smi/push.h:19-48
  * (implementation codegen/templates/push.cl:3-70): elements are packed into
- * packets (here 2032-byte payloads instead of 28-byte ones) and a packet is
+ * packets (here 16,368-byte payloads instead of 28-byte ones) and a packet is
  * sent when it is full, when the message is complete, or on an immediate
  * flush.  Sends are buffered (32 packets per communicator in flight), the
  * counterpart of the reference's credit window, so a rank may push before its
@@ -22,7 +22,7 @@ SMI_Channel SMI_Open_send_channel(int count, SMI_Datatype data_type, int destina
                                   SMI_Comm comm);
 /* asynch_degree (elements; the reference's channel FIFO depth,
  * codegen/rewrite.py:26-35): at most this many elements are packed before a
- * message leaves (capped at one 2032-byte payload); <= 0 = the default. */
+ * message leaves (capped at one 16,368-byte payload); <= 0 = the default. */
 SMI_Channel SMI_Open_send_channel_ad(int count, SMI_Datatype data_type, int destination, int port,
                                      SMI_Comm comm, int asynch_degree);
 void SMI_Push_flush(SMI_Channel *chan, void *data, int immediate);

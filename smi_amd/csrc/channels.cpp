@@ -6,7 +6,7 @@
 //   bcast.cl:3-149                    SMI_Bcast, root fan-out of packets
 //   reduce.cl:184-245                 SMI_Reduce, one element per packet
 //   scatter.cl:3-164 / gather.cl:3-162
-// Elements are packed into fixed-size messages (16-byte header + 2032-byte
+// Elements are packed into fixed-size messages (16-byte header + 16,368-byte
 // payload) that travel over the communicator's transport (RCCL over xGMI,
 // or the in-process device-copy transport).  Every message is tagged with its
 // port, and a per-communicator inbox demultiplexes them, so channels on
@@ -29,7 +29,11 @@
 namespace smi {
 namespace {
 
-constexpr size_t kMsgBytes = 2048;
+// A message costs about the same host and transport time at 2 KiB and at
+// 16 KiB (a host-to-device copy, the transport, a device-to-host copy and a
+// synchronisation on the receiver); 16 KiB streams 8x the elements per
+// message (profiles/r06/p2p/: element bandwidth 0.15 Gbit/s at 2 KiB).
+constexpr size_t kMsgBytes = 16384;
 constexpr size_t kHdrBytes = 16;
 constexpr size_t kPayload = kMsgBytes - kHdrBytes;
 constexpr int kSlots = 32;

@@ -150,7 +150,7 @@ def stencil_cases(comm, rank, world, s):
 
 def channel_cases(comm, rank, world, s):
     F = _lib.SMI_FLOAT
-    per_msg = 2032 // 4
+    per_msg = (16384 - 16) // 4
     partner = rank ^ 1
     if partner < world:
         # symmetric push-before-pop: both partners push 3 packets' worth, then pop

@@ -445,7 +445,7 @@ def test_stencil_host_under_torchrun(tmp_path):
 
 # ------------------------------------------------ point-to-point microbenchmarks --
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,kb,ranks,recv", [("bulk", 4096, 2, 1), ("bulk", 64, 3, 2), ("element", 16, 2, 1)])
+@pytest.mark.parametrize("mode,kb,ranks,recv", [("bulk", 4096, 2, 1), ("bulk", 64, 3, 2), ("element", 256, 2, 1)])
 def test_bandwidth_benchmark_host(tmp_path, mode, kb, ranks, recv):
     """bandwidth_0/1.cl: two ports of doubles 0.1f + i from rank 0 to the
     receiver, every element checked every run; threads as ranks."""

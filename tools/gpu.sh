@@ -16,6 +16,7 @@
 #             (STALL_US), host join vs wait packets
 #   fake      bench.py --gpus 2/4/8 --fake-host with parity (FAKE_N)
 #   hosts     the C++ hosts' tests (tests/test_hosts.py)
+#   p2p       tools/p2p_sweep.sh + a kernel trace of the 256 MiB bulk copy
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
@@ -89,6 +90,11 @@ for st in "$@"; do
       timeout -k 10 500 python bench.py --gpus $n --fake-host --steps 20 --warmup 5 --no-aux > $O/bench_fake$n.json 2> $O/bench_fake$n.err || fail fake$n $?
       python3 -c "import json;d=json.load(open('$O/bench_fake$n.json'));print('fake$n',d['value'],d['config']['decomposition'],d['parity']['bit_exact'],d['parity']['cells'])"
     done
+    ;;
+  p2p)
+    timeout -k 10 900 bash tools/p2p_sweep.sh $O/p2p || fail $st $?
+    (cd /tmp && TMPDIR=/tmp timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_p2p -o run -- $R/hosts/_build/bandwidth_benchmark -k 262144 -r 1 -i 10 -p 2 > $O/prof_p2p.log 2>&1) || fail prof_p2p $?
+    grep -h multicopy $O/prof_p2p/*kernel_stats.csv | head -2
     ;;
   *) echo "unknown step $st"; exit 2 ;;
   esac

@@ -19,7 +19,7 @@ step() {  # step <log name> <command...>
 for kb in 1 64 1024 16384 262144; do
   step bw_threads_bulk_$kb $B/bandwidth_benchmark -k $kb -r 1 -i 10 -p 2
 done
-step bw_threads_element_64 $B/bandwidth_benchmark -k 64 -r 1 -i 5 -p 2 -m element
+step bw_threads_element_1024 $B/bandwidth_benchmark -k 1024 -r 1 -i 5 -p 2 -m element
 step lat_threads_element $B/latency_benchmark -n 2000 -r 1 -i 10 -p 2
 step lat_threads_bulk $B/latency_benchmark -n 2000 -r 1 -i 10 -p 2 -m bulk
 port=$((29500 + RANDOM % 2000))
@@ -32,7 +32,7 @@ trstep() {  # trstep <log name> <host> <args...>: two processes under torchrun
 for kb in 1 64 1024 16384 262144; do
   trstep bw_procs_bulk_$kb $B/bandwidth_benchmark -k $kb -r 1 -i 10
 done
-trstep bw_procs_element_64 $B/bandwidth_benchmark -k 64 -r 1 -i 5 -m element
+trstep bw_procs_element_1024 $B/bandwidth_benchmark -k 1024 -r 1 -i 5 -m element
 trstep lat_procs_element $B/latency_benchmark -n 500 -r 1 -i 5
 trstep lat_procs_bulk $B/latency_benchmark -n 500 -r 1 -i 5 -m bulk
 echo done
