@@ -108,7 +108,9 @@ int send_msg(Comm *c, ChanEngine *e, int peer, int port, int kind, const char *p
     memcpy(h, &hdr, sizeof(hdr));
     memcpy(h + kHdrBytes, payload, (size_t)nelems * esz);
     SMI_HIP_CHECK(hipSetDevice(c->device));
-    SMI_HIP_CHECK(hipMemcpyAsync(d, h, kMsgBytes, hipMemcpyHostToDevice, e->send_stream));
+    // only the header and the elements cross to the device; the transport
+    // moves the whole fixed-size message (the tail is never read)
+    SMI_HIP_CHECK(hipMemcpyAsync(d, h, kHdrBytes + (size_t)nelems * esz, hipMemcpyHostToDevice, e->send_stream));
     return c->transport->send_detached(d, kMsgBytes, peer, e->send_stream, &e->tickets[slot]);
 }
 
@@ -131,7 +133,9 @@ int recv_msg(Comm *c, ChanEngine *e, int src, int port, int kind, Msg *out) {
         Msg m;
         m.kind = hdr.kind;
         m.nelems = hdr.nelems;
-        m.payload.assign(e->host_rslot + kHdrBytes, e->host_rslot + kMsgBytes);
+        // elements are at most 8 bytes (type_size): keep what the header covers
+        m.payload.assign(e->host_rslot + kHdrBytes,
+                         e->host_rslot + kHdrBytes + std::min(kPayload, (size_t)hdr.nelems * 8));
         e->inbox[{src, hdr.port}].push_back(std::move(m));
     }
     Msg &m = e->inbox[key].front();
