@@ -118,6 +118,41 @@ def test_asynch_degree_channels(gpu, ad):
     assert all(group(3, fn))
 
 
+ESZ = {CHAR: 1, SHORT: 2, INT: 4, FLOAT: 4, DOUBLE: 8}
+PAYLOAD = 16384 - 16  # channels.cpp: 16 KiB messages, 16-byte header
+
+
+@pytest.mark.parametrize("t", [CHAR, SHORT, INT, FLOAT, DOUBLE])
+def test_packet_boundaries(gpu, t):
+    """Counts at and around whole packets for every type (per packet:
+    16,368 bytes of elements): the last element of a full packet, the first
+    of the next, a lone element in a packet of its own; p2p and bcast."""
+    from smi_amd import channels as ch
+    per = PAYLOAD // ESZ[t]
+    counts = [per - 1, per, per + 1, 2 * per + 1]
+    mod = {CHAR: 127, SHORT: 32749}.get(t, 1 << 30)
+
+    def val(i):
+        return ch.NP[t](i % mod)
+
+    def fn(comm):
+        ok = True
+        for n in counts:
+            if comm.rank == 0:
+                c = ch.open_send_channel(n, t, 1, 3, comm)
+                for i in range(n):
+                    c.push(val(i))
+            else:
+                c = ch.open_receive_channel(n, t, 0, 3, comm)
+                ok &= all(c.pop() == val(i) for i in range(n))
+            b = ch.BChannel(n, t, 4, 0, comm)
+            got = [b.bcast(val(i) if comm.rank == 0 else 0) for i in range(n)]
+            ok &= all(g == val(i) for i, g in enumerate(got))
+        return ok
+
+    assert all(group(2, fn))
+
+
 def test_transient_channel_ends_after_count(gpu):
     from smi_amd import SMIError
     from smi_amd import channels as ch
