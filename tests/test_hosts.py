@@ -18,6 +18,10 @@ programs restated without Python in the loop.
   microbenchmarks (microbenchmarks/host/{bandwidth,latency}_benchmark.cpp with
   kernels/{bandwidth,latency}_{0,1}.cl): two ports of n doubles 0.1f + i, and
   an int ping-pong incremented on every round trip; element and bulk forms.
+* hosts/kmeans_smi_host.cpp -- examples/host/kmeans_smi.cpp:41-311: the
+  reference generator (libstdc++ minstd_rand0, seed 5) on rank 0, smi_bcast +
+  smi_scatter, one smi_kmeans per rank; centroids against the committed
+  golden fixtures and the oracle.
 
 Every host runs its ranks either as threads of one process (in-process
 group) or as one process per rank (--rank/--size/--uid, smi_init over RCCL,
@@ -82,7 +86,8 @@ def test_hosts_build_and_fail_loudly_without_gpu():
                  [_exe("broadcast_benchmark"), "-n", "16", "-r", "0", "-i", "1", "-p", "2"],
                  [_exe("gesummv_smi_host"), "-n", "64", "-m", "64", "-a", "1", "-c", "1", "-r", "1"],
                  [_exe("bandwidth_benchmark"), "-k", "1", "-r", "1", "-i", "1"],
-                 [_exe("latency_benchmark"), "-n", "4", "-r", "1", "-i", "1"]):
+                 [_exe("latency_benchmark"), "-n", "4", "-r", "1", "-i", "1"],
+                 [_exe("kmeans_smi_host"), "64", "1", "-p", "2", "-q"]):
         r = _run(args)
         assert r.returncode == 2, r.stdout + r.stderr
         assert "no GPU visible" in r.stderr
@@ -477,3 +482,56 @@ def test_p2p_benchmarks_processes(tmp_path, host, args):
     rcs, outs = _launch_ranks([_exe(host)] + args, 2, tmp_path)
     assert all(rc == 0 for rc in rcs), _log(rcs, outs)
     assert sum(o.count("Result is Ok!") for o in outs) == int(args[args.index("-i") + 1])
+
+
+# ------------------------------------------------------------------ kmeans_smi --
+def _golden_kmeans():
+    with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+        return json.load(f)["kmeans"]
+
+
+def test_kmeans_host_usage_errors():
+    """Usage errors exit 1 before any GPU work."""
+    exe = _exe("kmeans_smi_host")
+    assert _run([exe]).returncode == 1
+    assert _run([exe, "64", "1", "-w", "5", "-p", "2"]).returncode == 1   # 64 dims % 5
+    assert _run([exe, "63", "1", "-p", "2"]).returncode == 1              # 63 % 2 ranks
+
+
+@pytest.mark.gpu
+def test_kmeans_host_generator_overrun_stops():
+    """A num_points for which the reference's inclusive
+    uniform_int_distribution(0, num_points) picks one past the end of its
+    input (kmeans_smi.cpp:141-146; 8 points): exit 1, nothing read."""
+    r = _run([_exe("kmeans_smi_host"), "hardware", "8", "1", "-p", "1", "-q"])
+    assert r.returncode == 1 and "past the end" in r.stderr, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [0, 1])
+def test_kmeans_host_golden(tmp_path, case):
+    """The committed kmeans fixtures (tests/golden/golden.json: 2048 points on
+    8 ranks with W = 16, 10 iterations; 1536 points on 3 ranks with W = 1, 6
+    iterations), ranks as threads: final centroids bit-identical."""
+    g = _golden_kmeans()[case]
+    out = tmp_path / "cen.f32"
+    r = _run([_exe("kmeans_smi_host"), "emulator", str(g["num_points"]), str(g["iterations"]), "-k",
+              str(g["clusters"]), "-d", str(g["dims"]), "-w", str(g["width"]), "-p", str(g["ranks"]), "-o", str(out)])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Final centroids:" in r.stdout and r.stdout.count("Finished in") == g["ranks"]
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == g["sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_kmeans_host_processes_vs_oracle(tmp_path, world):
+    """One process per rank over RCCL: 4096 points of the reference generator,
+    W = 16, 6 iterations, bit-identical to the oracle's rank-order program."""
+    import oracle
+    out = tmp_path / "cen.f32"
+    rcs, outs = _launch_ranks([_exe("kmeans_smi_host"), "4096", "6", "-q", "-o", str(out)], world, tmp_path)
+    assert all(rc == 0 for rc in rcs), _log(rcs, outs)
+    _, pts, cen0 = oracle.kmeans_reference_data(4096, 8, 64)
+    want = oracle.kmeans(pts, cen0, 6, ranks=world, width=16)
+    got = np.fromfile(out, dtype=np.float32).reshape(want.shape)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
