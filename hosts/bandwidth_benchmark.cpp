@@ -64,7 +64,7 @@ bool element_port(SMI_Comm comm, bool sender, int peer, int port, int n) {
 int RankMain(SMI_Comm comm, const Args &a) {
     const int rank = SMI_Comm_rank(comm), ranks = SMI_Comm_size(comm);
     if (a.recv <= 0 || a.recv >= ranks) host::die(1, "receiver rank %d out of range for %d ranks\n", a.recv, ranks);
-    const int n = a.kb * 1024 / 8;
+    const int n = (int)((long)a.kb * 1024 / 8);  // kb < 2^24 (checked in main): n < 2^31
     hipStream_t stream;
     HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     host::Barrier barrier(comm, stream);
@@ -150,8 +150,8 @@ int main(int argc, char **argv) {
         }
     }
     const int ranks = launch.process() ? launch.size : a.ranks;
-    if (a.kb <= 0 || a.runs <= 0 || ranks < 2 || a.recv <= 0 || a.recv >= ranks) {
-        std::fprintf(stderr, "bad arguments (at least 2 ranks, receiver rank 1 .. ranks - 1)\n");
+    if (a.kb <= 0 || a.kb >= (1 << 24) || a.runs <= 0 || ranks < 2 || a.recv <= 0 || a.recv >= ranks) {
+        std::fprintf(stderr, "bad arguments (1 <= KiB < 2^24, at least 2 ranks, receiver rank 1 .. ranks - 1)\n");
         return 1;
     }
     return host::run_ranks(launch, a.ranks, [&](SMI_Comm comm) { return RankMain(comm, a); });
