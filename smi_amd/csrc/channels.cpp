@@ -17,6 +17,7 @@
 // contributions on the root with fold.h's fold_one, the same source as the
 // device fold kernel of smi_reduce.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -165,9 +166,9 @@ struct ChanState {
     std::vector<char> pkt;
     int fill = 0;
     long sent = 0;            // elements sent in the current segment
-    // unpacking (receive side), per source
-    std::map<int, Msg> cur;
-    std::map<int, int> pos;
+    // unpacking (receive side), per source rank (indexed, no lookup per element)
+    std::vector<Msg> cur;
+    std::vector<int> pos;
     // scatter / gather progress
     int next = 0;
     long seg = 0;
@@ -213,21 +214,41 @@ D open_desc(int kind, int count, int type, int peer, int port, SMI_Comm comm, in
     st->count = count;
     st->recv_count = recv_count;
     st->pkt.resize(kPayload);
+    st->cur.resize(c->size);
+    st->pos.assign(c->size, 0);
     std::lock_guard<std::mutex> lk(g_chan_mu);
     d.handle = g_next_chan++;
     g_chans[d.handle] = std::move(st);
     return d;
 }
 
+// Every element call looks its channel up.  A thread keeps its last lookup
+// and reuses it until any channel closes (the epoch moves under g_chan_mu):
+// a run of pushes or pops on one channel takes no lock.  Handles are never
+// reused.  A descriptor is used by one thread at a time, as its
+// processed_elements count already requires.
+std::atomic<unsigned> g_chan_epoch{0};
+struct ChanCache {
+    int handle = 0;
+    unsigned epoch = ~0u;
+    ChanState *s = nullptr;
+};
+thread_local ChanCache t_chan_cache;
+
 ChanState *state(int handle) {
+    ChanCache &cc = t_chan_cache;
+    if (cc.handle == handle && cc.epoch == g_chan_epoch.load(std::memory_order_acquire)) return cc.s;
     std::lock_guard<std::mutex> lk(g_chan_mu);
     auto it = g_chans.find(handle);
-    return it == g_chans.end() ? nullptr : it->second.get();
+    ChanState *s = it == g_chans.end() ? nullptr : it->second.get();
+    cc = ChanCache{handle, g_chan_epoch.load(std::memory_order_relaxed), s};
+    return s;
 }
 
 void close_chan(int *handle) {
     std::lock_guard<std::mutex> lk(g_chan_mu);
     g_chans.erase(*handle);
+    g_chan_epoch.fetch_add(1, std::memory_order_release);
     *handle = 0;
 }
 
